@@ -1,0 +1,287 @@
+"""Benchmark of the Stein-thinning hot path on MI355X (BASELINE.json metric).
+
+metric: Stein-kernel pair-evals/s + wall-clock to thin n=2e6 -> m=1e3, 1/2/4/8 GPU.
+A "step" = one complete greedy thin of the HBM-resident standardised sample (diagonal + m-1 fused
+kernel steps + argmin), i.e. n*m pair-evals; ms_per_step is the wall-clock of one thin.
+N = 1 workload: config 4 of BASELINE.json (LV surrogate, d=4, n=2e6, Langevin IMQ, 'med', m=1000).
+N > 1 (torchrun, one rank per GPU, RCCL): the same n rows sharded across ranks (strong scaling),
+one 16-B-per-rank-candidate all-gather per step.
+
+Synthetic data (no network): the LV posterior chains of the reference live only in S3, so the
+"LV surrogate" is a seeded random-walk Metropolis chain on N(mu, Sigma) with mu, Sigma the
+reference's printed LV chain-0 moments (Gradient_free.ipynb cells 42-43), isotropic step 0.0052
+tuned to the reference chains' acceptance rate 0.23 (Sampling.ipynb cells 16, 28: ~77% duplicated
+rows), ten pooled chains of 2e5 for n=2e6.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.join(ROOT, 'gradient-free-mcmc-postprocessing_amd')
+for _p in (ROOT, PKG_ROOT):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+BASELINE = json.load(open(os.path.join(ROOT, 'BASELINE.json')))
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+
+LV_MEAN = np.array([-0.38261842, 0.29176476, -0.02010969, -0.01824518])
+LV_COV = np.array([
+    [2.12987627e-04, 1.62995182e-04, -1.91636668e-04, -1.72343118e-04],
+    [1.62995182e-04, 1.97250184e-04, -1.02375977e-04, -6.37599091e-05],
+    [-1.91636668e-04, -1.02375977e-04, 2.16947410e-04, 2.13353024e-04],
+    [-1.72343118e-04, -6.37599091e-05, 2.13353024e-04, 2.30906788e-04],
+])
+CHAIN_LEN = 200_000
+RW_STEP = 0.0052   # acceptance ~0.23 as the reference RW-MH chains (Sampling.ipynb cell 28)
+
+
+def lv_surrogate(n: int, seed: int):
+    """Pooled seeded RW-MH chains on N(LV_MEAN, LV_COV) -> (x, grad log p, log p, (log q, grad log q))."""
+    from scipy.stats import multivariate_normal as mvn
+    rng = np.random.default_rng(seed)
+    chains = max(1, (n + CHAIN_LEN - 1) // CHAIN_LEN)
+    steps = (n + chains - 1) // chains
+    prec = np.linalg.inv(LV_COV)
+    d = LV_MEAN.shape[0]
+
+    def logp(z):
+        zc = z - LV_MEAN
+        return -0.5 * np.einsum('ij,jk,ik->i', zc, prec, zc)
+    cur = LV_MEAN + rng.multivariate_normal(np.zeros(d), LV_COV, size=chains)
+    lp = logp(cur)
+    out = np.empty((steps, chains, d))
+    noise = rng.normal(size=(steps, chains, d)) * RW_STEP
+    logu = np.log(rng.random(size=(steps, chains)))
+    for t in range(steps):
+        prop = cur + noise[t]
+        lpp = logp(prop)
+        acc = logu[t] < lpp - lp
+        cur = np.where(acc[:, None], prop, cur)
+        lp = np.where(acc, lpp, lp)
+        out[t] = cur
+    x = np.ascontiguousarray(out.transpose(1, 0, 2).reshape(-1, d)[:n])
+    grad = -(x - LV_MEAN) @ prec
+    log_p = mvn.logpdf(x, mean=LV_MEAN, cov=LV_COV)
+    mean = np.mean(x, axis=0)
+    cov = np.cov(x, rowvar=False, ddof=d)      # Gradient_free.ipynb cell 41 (ddof = d)
+    log_q = mvn.logpdf(x, mean=mean, cov=cov)
+    grad_q = -np.einsum('ij,kj->ki', np.linalg.inv(cov), x - mean)
+    return x, grad, log_p, (log_q, grad_q)
+
+
+def gaussian_d50(n: int, seed: int, d: int = 50, rho: float = 0.5):
+    """Config 5: iid N(0, AR(1) rho) in d=50; gradient-free with q = N(mean, 1.2 cov)."""
+    from scipy.stats import multivariate_normal as mvn
+    rng = np.random.default_rng(seed)
+    cov = rho ** np.abs(np.subtract.outer(np.arange(d), np.arange(d)))
+    x = rng.multivariate_normal(np.zeros(d), cov, size=n, method='cholesky')
+    log_p = mvn.logpdf(x, mean=np.zeros(d), cov=cov)
+    mean = np.mean(x, axis=0)
+    qcov = 1.2 * np.cov(x, rowvar=False)
+    log_q = mvn.logpdf(x, mean=mean, cov=qcov)
+    grad_q = -np.einsum('ij,kj->ki', np.linalg.inv(qcov), x - mean)
+    return x, log_p, log_q, grad_q
+
+
+CONFIGS = {
+    'c2': dict(desc='LV-surrogate d=4 n=2e5 Langevin IMQ med m=100', n=200_000, m=100, gf=False, seed=12347),
+    'c3': dict(desc='LV-surrogate d=4 n=2e5 gradient-free IMQ med m=100', n=200_000, m=100, gf=True, seed=12348),
+    'c4': dict(desc='LV-surrogate pooled d=4 n=2e6 Langevin IMQ med m=1000', n=2_000_000, m=1000, gf=False, seed=12345),
+    'c5': dict(desc='Gaussian AR(1) d=50 n=5e5 gradient-free IMQ med m=500', n=500_000, m=500, gf=True, seed=12349,
+               d50=True),
+}
+
+
+def make_integrand(cfg):
+    import warnings
+    from stein_thinning import thinning as st
+    if cfg.get('d50'):
+        x, log_p, log_q, gq = gaussian_d50(cfg['n'], cfg['seed'])
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            return st._make_stein_gf_integrand(x, log_p, log_q, gq, preconditioner='med'), x, None
+    x, g, log_p, (log_q, gq) = lv_surrogate(cfg['n'], cfg['seed'])
+    if cfg['gf']:
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            return st._make_stein_gf_integrand(x, log_p, log_q, gq, preconditioner='med'), x, (log_p, log_q, gq)
+    return st._make_stein_integrand(x, g, preconditioner='med'), x, g
+
+
+def cpu_baseline(cfg, integrand, steps: int):
+    """The NumPy restatement of the reference path (oracle/stein_numpy.py) on the same standardised
+    input, diagonal + `steps` greedy steps, timed on this host (NumPy ufuncs: 1 core)."""
+    from oracle import stein_numpy as ref
+    s, g, w = integrand.sample, integrand.gradient, integrand.weights
+    vfk0 = ref.make_imq(s, 'med')
+    if w is None:
+        def f(i1, i2):
+            return vfk0(s[i1], s[i2], g[i1], g[i2])
+    else:
+        def f(i1, i2):
+            return vfk0(s[i1], s[i2], g[i1], g[i2]) * w[i1] * w[i2]
+    t0 = time.perf_counter()
+    ref._greedy_search(steps + 1, f)
+    dt = time.perf_counter() - t0
+    pairs = cfg['n'] * (steps + 1)
+    return {'value': pairs / dt, 'unit': 'pair-evals/s', 'cores': 1, 'kind': 'port',
+            'sample': (f"oracle.stein_numpy._greedy_search (NumPy restatement of the reference path) on the "
+                       f"same standardised input, n={cfg['n']}, diagonal + {steps} steps = {pairs:.3g} pair-evals "
+                       f"in {dt:.1f} s; full m={cfg['m']} thin extrapolated: {cfg['n'] * cfg['m'] * dt / pairs:.0f} s; "
+                       f"NumPy {np.__version__}, single-threaded ufuncs, host {platform.processor() or platform.machine()} "
+                       f"({os.cpu_count()} logical CPUs)")}
+
+
+def kernel_timing(prob, n_points: int, repeats: int = 3):
+    """Average duration of the fused step kernel, measured with HIP events on the launch stream."""
+    import torch
+    from stein_thinning import _native as nat
+    L = nat.lib()
+    idx, a, ws = prob.greedy_buffers(n_points)
+    stride = int(L.st_candidate_stride(prob.d))
+    cands = torch.zeros(2 * stride, dtype=torch.float64, device=prob.x.device)
+    stream = torch.cuda.current_stream()
+    durs = []
+    for _ in range(repeats):
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_points)]
+        for t in range(n_points):
+            cin = cands[((t + 1) & 1) * stride:]
+            cout = cands[(t & 1) * stride:]
+            evs[t][0].record(stream)
+            nat.check(L.st_greedy_step(nat.ptr(prob.x), nat.ptr(prob.g), nat.ptr(prob.w), prob.n, prob.d, prob.ld,
+                                       prob.l, prob.tr, 0, t, 1, nat.ptr(cin), nat.ptr(cout), nat.ptr(idx),
+                                       nat.ptr(a), nat.ptr(ws), ws.numel() * 8, nat.stream_handle()), 'step')
+            evs[t][1].record(stream)
+        torch.cuda.synchronize()
+        durs.extend(e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs[1:])   # t >= 1: streaming steps
+    return float(np.mean(durs)), float(np.median(durs))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=5, help='timed thins')
+    ap.add_argument('--warmup', type=int, default=2)
+    ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
+    ap.add_argument('--cpu-steps', type=int, default=60, help='greedy steps of the CPU baseline sample')
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-kernel-timing', action='store_true')
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        dist.init_process_group('nccl', device_id=dev)
+
+    cfg = CONFIGS[args.config]
+    n, m = cfg['n'], cfg['m']
+    integrand, _, _ = make_integrand(cfg)
+    d = integrand.sample.shape[1]
+
+    if world == 1:
+        prob = integrand.device_problem()
+        idx, a, ws = prob.greedy_buffers(m)
+
+        def run_once():
+            prob.greedy_launch(m, idx, a, ws)
+    else:
+        from stein_thinning.distributed import HipShardBackend, run_sharded, shard_bounds
+        r0, r1 = shard_bounds(n, rank, world)
+        backend = HipShardBackend(integrand, r0, r1, world, m)
+
+        def run_once():
+            for t in range(m):
+                backend.step(t)
+                dist.all_gather_into_tensor(backend.recv, backend.send)
+            backend.finalize(m - 1)
+        _ = run_sharded
+
+    for _ in range(args.warmup):
+        run_once()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_once()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        dist.barrier()
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+
+    if world == 1:
+        result_idx = idx.cpu().numpy().view(np.uint32)
+    else:
+        result_idx = backend.indices()
+
+    roofline = None
+    cpu = None
+    if rank == 0:
+        bytes_per_pair = 16 * d + (24 if integrand.weights is not None else 16)
+        if world == 1 and not args.no_kernel_timing:
+            avg, med = kernel_timing(prob, min(m, 200))
+            alg_bytes = n * bytes_per_pair
+            achieved = alg_bytes / avg / 1e9
+            traffic = None
+            pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+            if os.path.exists(pmc):
+                rec = json.load(open(pmc)).get(args.config)
+                if rec:
+                    traffic = rec.get('hbm_bytes_per_launch')
+            roofline = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                        'kernel': f'greedy_step_ct<{d}>' if d <= 8 else 'greedy_step_rt',
+                        'kernel_avg_us': round(avg * 1e6, 2), 'kernel_median_us': round(med * 1e6, 2),
+                        'algorithmic_bytes_per_launch': alg_bytes,
+                        'bytes_per_pair': bytes_per_pair}
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(cfg, integrand, args.cpu_steps)
+
+    if rank == 0:
+        pairs = float(n) * m * args.steps
+        line = {
+            'metric': BASELINE['metric'],
+            'value': pairs / elapsed,
+            'unit': 'pair-evals/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': elapsed / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'strong',
+            'vs_baseline': None,
+            'dtype': 'f64',
+            'data': 'synthetic (seeded RW-MH LV-surrogate chains; see bench.py docstring)',
+            'config': {'workload': f"config {args.config[1]}: {cfg['desc']}", 'n': n, 'd': d, 'm': m,
+                       'preconditioner': 'med', 'kernel': 'gradient-free' if integrand.weights is not None else 'langevin',
+                       'parallelism': f'rows-sharded x{world}' if world > 1 else 'single-gpu',
+                       'wallclock_thin_s': elapsed / args.steps,
+                       'first_indices': result_idx[:8].tolist()},
+            'roofline': roofline,
+            'cpu_baseline': cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

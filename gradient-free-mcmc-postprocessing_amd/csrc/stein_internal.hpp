@@ -1,0 +1,63 @@
+// Internal (non-ABI) declarations shared by the HIP translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace st {
+
+constexpr int kMaxDim = 128;     // NumPy pairwise_sum modelled without recursion up to 128 lanes
+constexpr int kMaxCtDim = 8;     // compile-time-d kernels for d <= 8
+constexpr int kMaxBlocks = 1024; // greedy step grid cap (4 x 256-thread blocks per CU)
+constexpr int kCandHeader = 2;   // candidate record: {val, gidx(bits)} then x[d], g[d], w
+
+inline int64_t cand_stride(int d) { return ((kCandHeader + 2 * d + 1) + 1) & ~int64_t(1); }
+
+struct GreedyArgs {
+    const double* x;      // SoA (d, ld) standardised sample shard
+    const double* g;      // SoA (d, ld) standardised gradient (or gradient_q) shard
+    const double* w;      // (ld) gradient-free weights, or nullptr for the Langevin kernel
+    double* A;            // (ld) running sums, in place
+    int64_t n;            // rows in this shard
+    int64_t ld;           // leading dimension (even, >= n + (n & 1))
+    int d;
+    double l;             // isotropic preconditioner Gamma^-1 = l * I
+    double tr;            // np.trace(Gamma^-1), computed on the host exactly as the reference
+    int64_t row_offset;   // global index of shard row 0
+    const double* cands_in;  // R candidate records of the previous step (unused for the diagonal)
+    int nranks;
+    int64_t cand_stride;
+    double* cand_out;     // this rank's candidate record for this step
+    uint32_t* idx_out;    // device index array; launch t writes idx[t-1]
+    int64_t t;            // step being computed (0 = diagonal)
+    double* part_val;     // per-block partial MINLOC
+    int64_t* part_idx;
+    unsigned* ticket;     // monotone arrival counter, zeroed once per greedy run
+};
+
+int greedy_blocks(int64_t n, int d);
+hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, hipStream_t s);
+hipError_t launch_greedy_finalize(const double* cands, int nranks, int64_t stride,
+                                  uint32_t* idx_out, int64_t t, hipStream_t s);
+
+struct PairArgs {
+    const double* x;
+    const double* g;
+    const double* w;
+    int64_t ld;
+    int d;
+    double l;
+    double tr;
+};
+
+hipError_t launch_pairs(const PairArgs& p, const int64_t* i1, const int64_t* i2, int64_t L,
+                        double* out, hipStream_t s);
+hipError_t launch_ksd_rows(const PairArgs& p, const int64_t* idx, int64_t m, double* part,
+                           int64_t ntiles, hipStream_t s);
+hipError_t launch_ksd_scan(const double* part, int64_t m, int64_t ld, double* ks,
+                           hipStream_t s);
+hipError_t launch_kmat(const PairArgs& p, const int64_t* idx, int64_t k, double* out,
+                       hipStream_t s);
+hipError_t launch_layout_soa(const double* rowmajor, int64_t n, int d, int64_t ld, double* soa,
+                             hipStream_t s);
+
+}  // namespace st

@@ -1,0 +1,183 @@
+// Per-pair IMQ Stein-kernel arithmetic for gfx950 (fp64, VALU; no MFMA: pairwise scalar work).
+//
+// Reproduces, rounding for rounding, NumPy's evaluation of the reference's vfk0_imq
+// (restated at JAX_Stein_Thinning.ipynb cell 27, json ~354-361; maths report.tex:853-868) with an
+// isotropic preconditioner Gamma^-1 = l*I:
+//   qf  = 1 + SEQ_k fl(fl(l*dk)*dk)      t1 = fl(-3*SEQ_k fl(fl(l2*dk)*dk)) / qf^2.5
+//   t2  = fl(tr + SEQ_k fl(fl(l*(sa_k-sb_k))*dk)) / qf^1.5
+//   t3  = PAIRWISE_k fl(sa_k*sb_k) / sqrt(qf)        k = fl(fl(t1+t2)+t3)
+// SEQ = left-to-right (NumPy C-order axis-0 reduction), PAIRWISE = NumPy pairwise_sum.
+// The bit model is oracle/stein_ref.c; this file must stay in lock-step with it.
+// Compile with -ffp-contract=off: every mul/add above is a separately rounded op.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#pragma clang fp contract(off)
+
+namespace st {
+
+// correctly rounded (to ~2^-100) qf^1.5 and qf^2.5 from s = sqrt(qf) and its exact residual
+__device__ __forceinline__ void pow_15_25(double q, double& p15, double& p25, double& s) {
+    s = __builtin_sqrt(q);
+    const double e = __builtin_fma(-s, s, q);
+    const double c = e / (2.0 * s);
+    const double hi = q * s;
+    double lo = __builtin_fma(q, s, -hi);
+    lo = __builtin_fma(q, c, lo);
+    p15 = hi + lo;
+    const double q2 = q * q;
+    const double q2lo = __builtin_fma(q, q, -q2);
+    const double hi2 = q2 * s;
+    double lo2 = __builtin_fma(q2, s, -hi2);
+    lo2 = __builtin_fma(q2, c, lo2);
+    lo2 = __builtin_fma(q2lo, s, lo2);
+    p25 = hi2 + lo2;
+}
+
+__device__ __forceinline__ double finish_pair(double qs, double t1s, double t2s, double t3s,
+                                              double tr) {
+    const double qf = 1.0 + qs;
+    double p15, p25, s;
+    pow_15_25(qf, p15, p25, s);
+    const double t1 = (-3.0 * t1s) / p25;
+    const double t2 = (tr + t2s) / p15;
+    const double t3 = t3s / s;
+    return (t1 + t2) + t3;
+}
+
+// t3 follows NumPy pairwise_sum streamed over k (no product array): 0 + e0 + ... for d < 8;
+// 8 partial sums for 8 <= d <= 128.  (d > 128 rejected at the ABI.)
+
+// Compile-time d (D >= 1): everything unrolled, vectors in registers.
+template <int D>
+__device__ __forceinline__ double pair_value_ct(const double (&xi)[D], const double (&gi)[D],
+                                                const double* xj, const double* gj, double l,
+                                                double l2, double tr) {
+    double qs = 0.0, t1s = 0.0, t2s = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        const double dl = xi[k] - xj[k];
+        const double gd = gi[k] - gj[k];
+        const double q = (l * dl) * dl;
+        const double u = (l2 * dl) * dl;
+        const double v = (l * gd) * dl;
+        if (k == 0) {
+            qs = q; t1s = u; t2s = v;
+        } else {
+            qs = qs + q; t1s = t1s + u; t2s = t2s + v;
+        }
+    }
+    double t3s;
+    if constexpr (D < 8) {
+        t3s = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) t3s += gi[k] * gj[k];
+    } else {
+        static_assert(D <= 128, "pairwise_sum recursion not modelled beyond 128");
+        double r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = gi[k] * gj[k];
+        constexpr int full = D - (D % 8);
+#pragma unroll
+        for (int k = 8; k < full; ++k) r[k % 8] += gi[k] * gj[k];
+        t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+        for (int k = full; k < D; ++k) t3s += gi[k] * gj[k];
+    }
+    return finish_pair(qs, t1s, t2s, t3s, tr);
+}
+
+// Diagonal k(x, x) = fl(tr + PAIRWISE fl(g_k*g_k)) (dk = 0: qf = 1, t1 = -0, pow(1, .) = 1).
+template <int D>
+__device__ __forceinline__ double diag_value_ct(const double (&gi)[D], double tr) {
+    double t3s;
+    if constexpr (D < 8) {
+        t3s = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k) t3s += gi[k] * gi[k];
+    } else {
+        double r[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) r[k] = gi[k] * gi[k];
+        constexpr int full = D - (D % 8);
+#pragma unroll
+        for (int k = 8; k < full; ++k) r[k % 8] += gi[k] * gi[k];
+        t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+#pragma unroll
+        for (int k = full; k < D; ++k) t3s += gi[k] * gi[k];
+    }
+    // finish_pair(0, 0, 0, t3s): t1 = -0/1, t2 = tr/1, t3 = t3s/1 -> (-0 + tr) + t3s
+    return finish_pair(0.0, 0.0, 0.0, t3s, tr);
+}
+
+// Runtime d (1..128): point a strided by sa (SoA column: sa = ld), point b strided by sb.
+__device__ __forceinline__ double pair_value_rt(const double* __restrict__ xa,
+                                               const double* __restrict__ ga, int64_t sa,
+                                               const double* xb, const double* gb, int64_t sb,
+                                               int d, double l, double l2, double tr) {
+    double qs = 0.0, t1s = 0.0, t2s = 0.0;
+    double r[8];
+    double t3s = 0.0;
+    const int full = (d >= 8) ? d - (d % 8) : 0;
+    for (int k = 0; k < d; ++k) {
+        const double xak = xa[k * sa];
+        const double gak = ga[k * sa];
+        const double gbk = gb[k * sb];
+        const double dl = xak - xb[k * sb];
+        const double gd = gak - gbk;
+        const double q = (l * dl) * dl;
+        const double u = (l2 * dl) * dl;
+        const double v = (l * gd) * dl;
+        if (k == 0) {
+            qs = q; t1s = u; t2s = v;
+        } else {
+            qs = qs + q; t1s = t1s + u; t2s = t2s + v;
+        }
+        const double p = gak * gbk;
+        if (d < 8) {
+            t3s += p;
+        } else if (k < 8) {
+            r[k] = p;
+        } else if (k < full) {
+            r[k & 7] += p;
+        } else {
+            if (k == full) t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            t3s += p;
+        }
+    }
+    if (d >= 8 && full == d) t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    return finish_pair(qs, t1s, t2s, t3s, tr);
+}
+
+__device__ __forceinline__ double diag_value_rt(const double* __restrict__ gi_col, int64_t ld,
+                                                int d, double tr) {
+    double r[8];
+    double t3s = 0.0;
+    const int full = (d >= 8) ? d - (d % 8) : 0;
+    for (int k = 0; k < d; ++k) {
+        const double gik = gi_col[k * ld];
+        const double p = gik * gik;
+        if (d < 8) {
+            t3s += p;
+        } else if (k < 8) {
+            r[k] = p;
+        } else if (k < full) {
+            r[k & 7] += p;
+        } else {
+            if (k == full) t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+            t3s += p;
+        }
+    }
+    if (d >= 8 && full == d) t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    return finish_pair(0.0, 0.0, 0.0, t3s, tr);
+}
+
+// np.argmin order: NaN is the minimum (first NaN wins), otherwise smaller value, ties -> lower index
+__device__ __forceinline__ bool better(double a, int64_t ia, double b, int64_t ib) {
+    const bool na = __builtin_isnan(a), nb = __builtin_isnan(b);
+    if (na | nb) return na && (!nb || ia < ib);
+    return (a < b) || (a == b && ia < ib);
+}
+
+}  // namespace st

@@ -1,0 +1,111 @@
+"""ctypes binding of the HIP C-ABI (include/stein_thinning_hip.h).
+
+The shared library ``_lib/libstein_hip.so`` is built in-tree by ``__graft_entry__.build()``
+(hipcc --offload-arch=gfx950).  Nothing here touches HIP at import time (the reference calls the
+library from joblib / Dask worker processes, ``code/src/utils/parallel.py:18-52``); the library is
+loaded on first use, after ``torch`` so that exactly one HIP runtime (torch's
+``libamdhip64.so.7``) is mapped into the process.  There is no CPU fallback: every entry point
+raises if the extension or a HIP device is missing.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_LIB = None
+_LOCK = threading.Lock()
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), '_lib', 'libstein_hip.so')
+
+ST_OK = 0
+ST_ERR_INVALID = -1
+ST_ERR_UNSUPPORTED = -2
+ST_ERR_HIP = -3
+
+_c_dp = ctypes.c_void_p  # device pointers / stream handles
+_i64 = ctypes.c_int64
+_i32 = ctypes.c_int32
+_f64 = ctypes.c_double
+
+# symbol -> (restype, argtypes); mirrors include/stein_thinning_hip.h
+SIGNATURES = {
+    'st_abi_version': (ctypes.c_int, []),
+    'st_last_error': (ctypes.c_char_p, []),
+    'st_greedy_workspace_bytes': (_i64, [_i64, _i32, _i32]),
+    'st_candidate_stride': (_i64, [_i32]),
+    'st_greedy': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64, _i64,
+                                 _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
+    'st_greedy_step': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
+                                      _i64, _i64, _i32, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
+                                      _i64, _c_dp]),
+    'st_greedy_finalize': (ctypes.c_int, [_c_dp, _i32, _i32, _c_dp, _i64, _c_dp]),
+    'st_kernel_pairs': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _f64, _f64, _c_dp,
+                                       _c_dp, _i64, _c_dp, _c_dp]),
+    'st_ksd_workspace_bytes': (_i64, [_i64, _i64]),
+    'st_ksd_cumulative': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i64, _i32, _f64, _f64,
+                                         _c_dp, _c_dp, _i64, _c_dp]),
+    'st_kmat': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i64, _i32, _f64, _f64, _c_dp,
+                               _c_dp]),
+    'st_layout_soa': (ctypes.c_int, [_c_dp, _i64, _i32, _i64, _c_dp, _c_dp]),
+}
+ABI_VERSION = 1
+
+
+class HipExtensionError(RuntimeError):
+    """The HIP extension is missing, failed to load, or reported an error."""
+
+
+def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load and type the C-ABI library (no GPU access: usable for symbol checks on CPU hosts)."""
+    if not os.path.exists(path):
+        raise HipExtensionError(
+            f'HIP extension not built: {path} is missing. Run `python -c "import __graft_entry__ as g; '
+            f'g.build()"` from the repository root (hipcc --offload-arch=gfx950).')
+    lib = ctypes.CDLL(path)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    if lib.st_abi_version() != ABI_VERSION:
+        raise HipExtensionError(f'ABI mismatch: library {lib.st_abi_version()} != {ABI_VERSION}')
+    return lib
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        with _LOCK:
+            if _LIB is None:
+                import torch  # noqa: F401  -- map torch's HIP runtime before ours resolves against it
+                _LIB = load_library()
+    return _LIB
+
+
+def check(rc: int, what: str = '') -> None:
+    if rc != ST_OK:
+        msg = lib().st_last_error().decode(errors='replace')
+        if rc == ST_ERR_UNSUPPORTED:
+            raise NotImplementedError(f'{what}: {msg}')
+        if rc == ST_ERR_INVALID:
+            raise ValueError(f'{what}: {msg}')
+        raise HipExtensionError(f'{what}: HIP error ({rc}): {msg}')
+
+
+def require_device():
+    """Return the torch device the engine runs on; raise if no HIP device is visible."""
+    import torch
+    if not torch.cuda.is_available():
+        raise HipExtensionError(
+            'stein_thinning (MI355X engine) needs a HIP device: torch.cuda.is_available() is False. '
+            'There is no CPU fallback.')
+    return torch.device('cuda', torch.cuda.current_device())
+
+
+def stream_handle():
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)

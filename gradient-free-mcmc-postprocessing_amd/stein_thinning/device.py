@@ -1,0 +1,153 @@
+"""HBM-resident problem: the standardised sample / score (SoA fp64) plus optional weights.
+
+Data layout in HBM (DESIGN.md "Data layout"): element (i, k) of an (n, d) array lives at
+``soa[k * ld + i]`` with ``ld`` = n rounded up to a multiple of 64, so that every candidate column
+is a coalesced, 512-byte-aligned fp64 stream and a lane reads two adjacent candidates with one
+16-byte load.  Weights and running sums are (ld,) vectors.  Padding rows are zero and never enter
+an argmin.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import numpy as np
+
+from . import _native as nat
+
+PAD = 64
+
+
+def padded_ld(n: int) -> int:
+    return max(PAD, ((n + PAD - 1) // PAD) * PAD)
+
+
+def isotropic_scale(linv: np.ndarray):
+    """(l, trace) if linv == l * I exactly, else None (dense preconditioners: not on the HIP path)."""
+    linv = np.asarray(linv, dtype=np.float64)
+    d = linv.shape[0]
+    diag = np.diag(linv)
+    off = linv - np.diag(diag)
+    if np.any(off != 0) or np.any(diag != diag[0]):
+        return None
+    # np.trace(linv) exactly as the reference evaluates it (pairwise for d >= 8)
+    return float(diag[0]), float(np.trace(linv))
+
+
+class DeviceProblem:
+    """Standardised (n, d) sample + score resident on the GPU in SoA layout."""
+
+    def __init__(self, sample: np.ndarray, gradient: np.ndarray, weights: Optional[np.ndarray],
+                 linv_scale: float, linv_trace: float, device=None):
+        import torch
+        self.device = device if device is not None else nat.require_device()
+        sample = np.ascontiguousarray(sample, dtype=np.float64)
+        gradient = np.ascontiguousarray(gradient, dtype=np.float64)
+        self.n, self.d = sample.shape
+        if self.d > 128:
+            raise NotImplementedError(f'd = {self.d} > 128 is not supported by the HIP engine')
+        self.ld = padded_ld(self.n)
+        self.l = float(linv_scale)
+        self.tr = float(linv_trace)
+        self.x = self._soa(torch, sample)
+        self.g = self._soa(torch, gradient)
+        self.w = None
+        if weights is not None:
+            w = torch.zeros(self.ld, dtype=torch.float64, device=self.device)
+            w[:self.n] = torch.from_numpy(np.ascontiguousarray(weights, dtype=np.float64)).to(self.device)
+            self.w = w
+
+    def _soa(self, torch, rowmajor: np.ndarray):
+        rm = torch.from_numpy(rowmajor).to(self.device, non_blocking=False)
+        soa = torch.zeros((self.d, self.ld), dtype=torch.float64, device=self.device)
+        nat.check(nat.lib().st_layout_soa(nat.ptr(rm), self.n, self.d, self.ld, nat.ptr(soa),
+                                          nat.stream_handle()), 'st_layout_soa')
+        return soa
+
+    @classmethod
+    def from_soa(cls, x_soa, g_soa, w, n: int, linv_scale: float, linv_trace: float):
+        """Wrap already-resident SoA tensors (d, ld) without copies (bench / sharded paths)."""
+        self = cls.__new__(cls)
+        self.device = x_soa.device
+        self.d, self.ld = x_soa.shape
+        self.n = int(n)
+        self.l, self.tr = float(linv_scale), float(linv_trace)
+        self.x, self.g, self.w = x_soa, g_soa, w
+        return self
+
+    # -- greedy ------------------------------------------------------------------------------
+    def greedy_buffers(self, n_points: int):
+        import torch
+        ws_bytes = int(nat.lib().st_greedy_workspace_bytes(self.n, self.d, 1))
+        ws = torch.empty((ws_bytes + 15) // 16 * 2, dtype=torch.float64, device=self.device)
+        a = torch.empty(self.ld, dtype=torch.float64, device=self.device)
+        idx = torch.empty(n_points, dtype=torch.int32, device=self.device)
+        return idx, a, ws
+
+    def greedy_launch(self, n_points: int, idx, a, ws) -> None:
+        """Enqueue the whole greedy run on the current stream (no sync)."""
+        nat.check(nat.lib().st_greedy(
+            nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.n, self.d, self.ld,
+            self.l, self.tr, int(n_points), nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
+            ws.numel() * 8, nat.stream_handle()), 'st_greedy')
+
+    def greedy(self, n_points: int, return_sums: bool = False):
+        idx, a, ws = self.greedy_buffers(n_points)
+        self.greedy_launch(n_points, idx, a, ws)
+        out = idx.cpu().numpy().view(np.uint32).copy()
+        if return_sums:
+            return out, a[:self.n].cpu().numpy()
+        return out
+
+    # -- integrand protocol --------------------------------------------------------------------
+    def pairs(self, i1: np.ndarray, i2: np.ndarray) -> np.ndarray:
+        import torch
+        L = int(i1.shape[0])
+        if L == 0:
+            return np.empty(0, dtype=np.float64)
+        t1 = torch.from_numpy(np.ascontiguousarray(i1, dtype=np.int64)).to(self.device)
+        t2 = torch.from_numpy(np.ascontiguousarray(i2, dtype=np.int64)).to(self.device)
+        out = torch.empty(L, dtype=torch.float64, device=self.device)
+        nat.check(nat.lib().st_kernel_pairs(
+            nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.ld, self.d, self.l, self.tr,
+            nat.ptr(t1), nat.ptr(t2), L, nat.ptr(out), nat.stream_handle()), 'st_kernel_pairs')
+        return out.cpu().numpy()
+
+    def subset(self, rows: np.ndarray) -> 'DeviceProblem':
+        """Compact problem of the given rows (gather on device; used by ksd / kmat)."""
+        import torch
+        rows = np.asarray(rows, dtype=np.int64).reshape(-1)
+        m = rows.shape[0]
+        ld = padded_ld(m)
+        ti = torch.from_numpy(rows).to(self.device)
+        x = torch.zeros((self.d, ld), dtype=torch.float64, device=self.device)
+        g = torch.zeros((self.d, ld), dtype=torch.float64, device=self.device)
+        x[:, :m] = self.x.index_select(1, ti)
+        g[:, :m] = self.g.index_select(1, ti)
+        w = None
+        if self.w is not None:
+            w = torch.zeros(ld, dtype=torch.float64, device=self.device)
+            w[:m] = self.w.index_select(0, ti)
+        return DeviceProblem.from_soa(x, g, w, m, self.l, self.tr)
+
+    def ksd(self, m: int) -> np.ndarray:
+        """Cumulative KSD over rows 0..m-1 of this problem."""
+        import torch
+        if m == 0:
+            return np.empty(0)
+        ws_bytes = int(nat.lib().st_ksd_workspace_bytes(m, self.ld))
+        ws = torch.empty((ws_bytes + 7) // 8, dtype=torch.float64, device=self.device)
+        ks = torch.empty(m, dtype=torch.float64, device=self.device)
+        nat.check(nat.lib().st_ksd_cumulative(
+            nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), m, self.ld, self.d, self.l, self.tr,
+            nat.ptr(ks), nat.ptr(ws), ws.numel() * 8, nat.stream_handle()), 'st_ksd_cumulative')
+        return ks.cpu().numpy()
+
+    def kmat(self, k: int) -> np.ndarray:
+        import torch
+        if k == 0:
+            return np.zeros((0, 0))
+        out = torch.empty((k, k), dtype=torch.float64, device=self.device)
+        nat.check(nat.lib().st_kmat(
+            nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), k, self.ld, self.d, self.l, self.tr,
+            nat.ptr(out), nat.stream_handle()), 'st_kmat')
+        return out.cpu().numpy()

@@ -1,0 +1,117 @@
+/*
+ * stein_thinning_hip.h -- C ABI of the MI355X (gfx950) Stein-thinning engine.
+ *
+ * Drop-in boundary for the hot path of the reference's third-party dependency `stein_thinning`
+ * (imported at code/src/thinning.py:5, code/src/utils/ksd.py:5-6, code/tests/test_ksd.py:3 of
+ * aglebov/gradient-free-mcmc-postprocessing).  The Python shim package `stein_thinning`
+ * (gradient-free-mcmc-postprocessing_amd/stein_thinning) binds these symbols with ctypes; see
+ * INTEGRATION.md for the binding a maintainer adds.
+ *
+ * Conventions (all functions):
+ *   - plain C types only; device pointers are HIP device memory owned by the caller;
+ *   - `stream` is a hipStream_t (NULL = default stream); every function is asynchronous on it,
+ *     allocates nothing and never synchronises (graph-capturable);
+ *   - sample / gradient arrays are SoA: element (i, k) of the (n, d) array lives at p[k * ld + i],
+ *     ld even and >= n + (n & 1); per-row arrays (weights, running sums) have ld entries;
+ *     all device pointers 16-byte aligned;
+ *   - the preconditioner is isotropic Gamma^-1 = linv_scale * I ('id', 'med', 'sclmed', float
+ *     options of the reference); linv_trace = np.trace(Gamma^-1) computed on the host;
+ *   - weights == NULL selects the Langevin Stein kernel k_P; weights = w = exp(log q - log p)
+ *     (anchored) selects the gradient-free kernel k_PQ(i,j) = w_i w_j k_Q(i,j) (report.tex:390-400);
+ *   - return value: ST_OK (0) or a negative ST_ERR_*; st_last_error() describes the last failure
+ *     of the calling thread.  No C++ exception crosses the ABI.
+ */
+#ifndef STEIN_THINNING_HIP_H
+#define STEIN_THINNING_HIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ST_ABI_VERSION 1
+
+#define ST_OK 0
+#define ST_ERR_INVALID (-1)     /* bad argument: sizes, null pointers, alignment */
+#define ST_ERR_UNSUPPORTED (-2) /* e.g. d > 128 */
+#define ST_ERR_HIP (-3)         /* HIP runtime error (launch / memset) */
+
+int st_abi_version(void);
+const char *st_last_error(void);
+
+/* ------------------------------------------------------------------------------------------
+ * Greedy selection -- replaces stein_thinning.thinning._greedy_search(n_points, integrand)
+ * (restated at code/notebooks/examples/JAX_Stein_Thinning.ipynb cell 22, json lines ~281-295;
+ * Algorithm 3, report/report.tex:413-426) for the integrands built by _make_stein_integrand /
+ * _make_stein_gf_integrand (called at code/src/utils/ksd.py:25, Gaussian_mixture.ipynb cell 93).
+ * ---------------------------------------------------------------------------------------- */
+
+/* bytes of device workspace st_greedy / st_greedy_step need (zeroing is done internally) */
+int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
+
+/* doubles per rank-candidate record {value, global index bits, x[d], g[d], w} (even) */
+int64_t st_candidate_stride(int32_t d);
+
+/*
+ * Whole greedy run on one device: idx_out[0..n_points) (device, uint32) receives the selected
+ * row indices exactly as the reference's `thin` / `thin_gf` / `_greedy_search` return them;
+ * a_work (ld doubles, device) ends holding the running sums A after the last step.
+ */
+int st_greedy(const double *x_soa, const double *g_soa, const double *weights, int64_t n,
+              int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t n_points,
+              uint32_t *idx_out, double *a_work, void *workspace, int64_t workspace_bytes,
+              void *stream);
+
+/*
+ * One greedy step of a row-sharded run (multi-GPU; one process per GPU).  This rank holds rows
+ * [row_offset, row_offset + n) of the global sample.  Step t = 0 evaluates the diagonal; step
+ * t >= 1 reads the R = nranks candidate records of step t-1 (cands_in, R * stride doubles),
+ * writes idx_out[t-1] and updates the running sums.  Every step writes this rank's candidate
+ * record to cand_out; the caller all-gathers the records (RCCL) into the next step's cands_in.
+ * After the last step, st_greedy_finalize writes idx_out[n_points-1].
+ */
+int st_greedy_step(const double *x_soa, const double *g_soa, const double *weights, int64_t n,
+                   int32_t d, int64_t ld, double linv_scale, double linv_trace,
+                   int64_t row_offset, int64_t t, int32_t nranks, const double *cands_in,
+                   double *cand_out, uint32_t *idx_out, double *a_work, void *workspace,
+                   int64_t workspace_bytes, void *stream);
+
+int st_greedy_finalize(const double *cands_in, int32_t nranks, int32_t d, uint32_t *idx_out,
+                       int64_t t, void *stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Integrand protocol -- replaces integrand(ind1, ind2) of the closures returned by
+ * stein_thinning.thinning._make_stein_integrand / _make_stein_gf_integrand and
+ * stein_thinning.kernel.vfk0_imq (restated at JAX_Stein_Thinning.ipynb cell 27, json ~354-361;
+ * Kernel_Stein_discrepancy.ipynb cell 7): out[p] = k(row i1[p], row i2[p]) (weights: w_i1 w_i2).
+ * ---------------------------------------------------------------------------------------- */
+int st_kernel_pairs(const double *x_soa, const double *g_soa, const double *weights, int64_t ld,
+                    int32_t d, double linv_scale, double linv_trace, const int64_t *i1,
+                    const int64_t *i2, int64_t n_pairs, double *out, void *stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Kernel Stein discrepancy -- replaces stein_thinning.stein.ksd(integrand, n) (called at
+ * code/src/utils/ksd.py:27 via calculate_ksd; Gaussian_mixture.ipynb cell 83) and
+ * stein_thinning.stein.kmat(integrand, n) (code/tests/test_ksd.py:20; Gaussian_mixture.ipynb
+ * cell 94).  Both take a COMPACT problem of m (k) rows (gather the selected rows first).
+ * ks_out[i] = sqrt(sum_{a,b <= i} k(a,b)) / (i+1).  kmat_out is the full symmetric (k, k)
+ * row-major matrix K[r][c] = k(min(r,c), max(r,c)).
+ * ---------------------------------------------------------------------------------------- */
+int64_t st_ksd_workspace_bytes(int64_t m, int64_t ld);
+int st_ksd_cumulative(const double *x_soa, const double *g_soa, const double *weights, int64_t m,
+                      int64_t ld, int32_t d, double linv_scale, double linv_trace, double *ks_out,
+                      void *workspace, int64_t workspace_bytes, void *stream);
+int st_kmat(const double *x_soa, const double *g_soa, const double *weights, int64_t k,
+            int64_t ld, int32_t d, double linv_scale, double linv_trace, double *kmat_out,
+            void *stream);
+
+/* row-major (n, d) -> SoA (d, ld) layout helper (device to device) */
+int st_layout_soa(const double *rowmajor, int64_t n, int32_t d, int64_t ld, double *soa,
+                  void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* STEIN_THINNING_HIP_H */

@@ -1,0 +1,146 @@
+/*
+ * C restatement of the reference Stein-thinning hot path -- TEST INFRASTRUCTURE ONLY.
+ *
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load this (as the
+ * checker).  It is the *bit model* of the HIP kernels: the per-pair arithmetic follows NumPy's
+ * evaluation order of the reference's vfk0_imq (JAX_Stein_Thinning.ipynb cell 27, json ~354-361;
+ * see oracle/stein_numpy.py), verified bit-for-bit against NumPy in tests/test_oracle_bitmodel.py:
+ *
+ *   delta_k = a_k - b_k
+ *   qf  = 1 + SEQ_k fl(fl(l  * delta_k) * delta_k)          np.sum(np.dot(linv, amb) * amb, axis=0)
+ *   t1s =     SEQ_k fl(fl(l2 * delta_k) * delta_k)          l2 = fl(l*l) = diag(linv @ linv)
+ *   t2s =     SEQ_k fl(fl(l * (sa_k - sb_k)) * delta_k)
+ *   t3s =     PAIRWISE_k fl(sa_k * sb_k)                     (NumPy pairwise_sum: 8 lanes, d >= 8)
+ *   k   = fl(fl(fl(-3*t1s) / qf^2.5) + fl(fl(tr + t2s) / qf^1.5)) + fl(t3s / sqrt(qf))
+ *
+ * SEQ = sequential left-to-right adds (C-contiguous axis-0 reduction); PAIRWISE = NumPy's
+ * pairwise_sum (res = 0 + e0 + ... for d < 8; 8 partial sums, ((r0+r1)+(r2+r3))+((r4+r5)+(r6+r7)),
+ * then the remainder, for 8 <= d <= 128).  qf^1.5 and qf^2.5 are evaluated correctly rounded
+ * (double-double around the correctly rounded sqrt); NumPy's own SIMD pow is within 1 ulp of that
+ * (it is not bit-reproducible across CPUs either -- DESIGN.md "pow").
+ *
+ * Gradient-free: k_PQ(i, j) = fl(fl(k * w_i) * w_j) (reference integrand * weights[ind1] * weights[ind2]).
+ * Greedy: A = diag; idx0 = argmin A; A = fl(A + 2*col); first minimum, NaN counts as minimum
+ * (np.argmin) -- JAX_Stein_Thinning.ipynb cell 22 (~281-295), report.tex:413-426.
+ *
+ * Build: gcc -O2 -fPIC -shared -ffp-contract=off -o oracle/_build/libstein_ref.so oracle/stein_ref.c -lm
+ */
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+
+static double pairwise_sum(const double *v, int64_t n) {
+    if (n < 8) {
+        double res = 0.;
+        for (int64_t i = 0; i < n; i++) res += v[i];
+        return res;
+    } else if (n <= 128) {
+        double r[8], res;
+        int64_t i;
+        for (int j = 0; j < 8; j++) r[j] = v[j];
+        for (i = 8; i < n - (n % 8); i += 8)
+            for (int j = 0; j < 8; j++) r[j] += v[i + j];
+        res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+        for (; i < n; i++) res += v[i];
+        return res;
+    } else {
+        int64_t n2 = n / 2;
+        n2 -= n2 % 8;
+        return pairwise_sum(v, n2) + pairwise_sum(v + n2, n - n2);
+    }
+}
+
+/* correctly rounded qf^1.5, qf^2.5 via s = sqrt(qf) and its exact residual */
+static void pow_15_25(double q, double *p15, double *p25, double *sq) {
+    double s = sqrt(q);
+    double e = fma(-s, s, q);
+    double c = e / (2.0 * s);
+    double hi = q * s;
+    double lo = fma(q, s, -hi);
+    lo = fma(q, c, lo);
+    *p15 = hi + lo;
+    double q2 = q * q;
+    double q2lo = fma(q, q, -q2);
+    double hi2 = q2 * s;
+    double lo2 = fma(q2, s, -hi2);
+    lo2 = fma(q2, c, lo2);
+    lo2 = fma(q2lo, s, lo2);
+    *p25 = hi2 + lo2;
+    *sq = s;
+}
+
+/* one Stein-kernel value; a/b/sa/sb are d-vectors with strides */
+static double pair_value(const double *a, int64_t sa_stride, const double *b, int64_t sb_stride,
+                         const double *ga, const double *gb, int d, double l, double tr) {
+    double l2 = l * l;
+    double prod[128];
+    double qs = 0, t1s = 0, t2s = 0;
+    for (int k = 0; k < d; k++) {
+        double dl = a[k * sa_stride] - b[k * sb_stride];
+        double gd = ga[k * sa_stride] - gb[k * sb_stride];
+        double q = (l * dl) * dl;
+        double u = (l2 * dl) * dl;
+        double v = (l * gd) * dl;
+        if (k == 0) { qs = q; t1s = u; t2s = v; }
+        else { qs = qs + q; t1s = t1s + u; t2s = t2s + v; }
+        prod[k] = ga[k * sa_stride] * gb[k * sb_stride];
+    }
+    double t3s = pairwise_sum(prod, d);
+    double qf = 1.0 + qs;
+    double p15, p25, s;
+    pow_15_25(qf, &p15, &p25, &s);
+    double t1 = (-3.0 * t1s) / p25;
+    double t2 = (tr + t2s) / p15;
+    double t3 = t3s / s;
+    return (t1 + t2) + t3;
+}
+
+static int better(double a, int64_t ia, double b, int64_t ib) {
+    if (isnan(a)) return isnan(b) ? (ia < ib) : 1;
+    if (isnan(b)) return 0;
+    return (a < b) || (a == b && ia < ib);
+}
+
+/*
+ * x, g: row-major (n, d); w: weights or NULL; A: (n) running sums (out); idx: (m) out.
+ * Returns 0 on success, -1 on unsupported d.
+ */
+int sr_greedy(const double *x, const double *g, const double *w, int64_t n, int d,
+              double l, double tr, int64_t m, uint32_t *idx, double *A) {
+    if (d < 1 || d > 128) return -1;
+    for (int64_t i = 0; i < n; i++) {
+        double k = pair_value(x + i * d, 1, x + i * d, 1, g + i * d, g + i * d, d, l, tr);
+        if (w) k = (k * w[i]) * w[i];
+        A[i] = k;
+    }
+    for (int64_t t = 0; t < m; t++) {
+        if (t > 0) {
+            int64_t j = idx[t - 1];
+            for (int64_t i = 0; i < n; i++) {
+                double k = pair_value(x + i * d, 1, x + j * d, 1, g + i * d, g + j * d, d, l, tr);
+                if (w) k = (k * w[i]) * w[j];
+                A[i] = A[i] + 2.0 * k;
+            }
+        }
+        int64_t best = 0;
+        for (int64_t i = 1; i < n; i++)
+            if (better(A[i], i, A[best], best)) best = i;
+        idx[t] = (uint32_t)best;
+    }
+    return 0;
+}
+
+/* pair values out[p] = k(i1[p], i2[p]) with weights fl(fl(k*w_i1)*w_i2) */
+int sr_pairs(const double *x, const double *g, const double *w, int64_t n, int d, double l, double tr,
+             const int64_t *i1, const int64_t *i2, int64_t L, double *out) {
+    (void)n;
+    if (d < 1 || d > 128) return -1;
+    for (int64_t p = 0; p < L; p++) {
+        int64_t a = i1[p], b = i2[p];
+        double k = pair_value(x + a * d, 1, x + b * d, 1, g + a * d, g + b * d, d, l, tr);
+        if (w) k = (k * w[a]) * w[b];
+        out[p] = k;
+    }
+    return 0;
+}

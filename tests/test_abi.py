@@ -1,0 +1,60 @@
+"""The C-ABI library loads (no GPU needed) and exports every function include/*.h declares."""
+import glob
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _declared():
+    names = set()
+    for h in glob.glob(os.path.join(ROOT, 'include', '*.h')):
+        src = open(h).read()
+        src = re.sub(r'/\*.*?\*/', '', src, flags=re.S)
+        names |= set(re.findall(r'^\s*(?:const\s+)?[A-Za-z_][A-Za-z0-9_]*\s*\**\s*(st_[a-z0-9_]+)\s*\(', src, flags=re.M))
+    return names
+
+
+@pytest.fixture(scope='module')
+def libpath():
+    import __graft_entry__ as ge
+    ge.build()
+    return ge.HIP_LIB
+
+
+def test_header_declares_api():
+    names = _declared()
+    for must in ['st_greedy', 'st_greedy_step', 'st_greedy_finalize', 'st_kernel_pairs', 'st_ksd_cumulative',
+                 'st_kmat', 'st_last_error', 'st_abi_version', 'st_layout_soa']:
+        assert must in names
+
+
+def test_library_exports_every_declared_symbol(libpath):
+    out = subprocess.run(['nm', '-D', '--defined-only', libpath], capture_output=True, text=True, check=True).stdout
+    exported = {ln.split()[-1] for ln in out.splitlines() if ln.strip()}
+    missing = _declared() - exported
+    assert not missing, missing
+
+
+def test_library_loads_and_types_without_gpu(libpath):
+    from stein_thinning import _native
+    lib = _native.load_library(libpath)
+    assert lib.st_abi_version() == _native.ABI_VERSION
+    assert set(_native.SIGNATURES) == _declared()
+    # host-only entry points: sizes and argument validation (no device memory touched)
+    assert lib.st_candidate_stride(4) == 12
+    assert lib.st_greedy_workspace_bytes(10, 4, 1) > 0
+    assert lib.st_greedy_workspace_bytes(10, 129, 1) == -1
+    assert lib.st_greedy(None, None, None, 10, 4, 10, 1.0, 4.0, 5, None, None, None, 0, None) == _native.ST_ERR_INVALID
+    assert b'NULL' in lib.st_last_error()
+    assert lib.st_kernel_pairs(None, None, None, 8, 200, 1.0, 1.0, None, None, 1, None, None) == _native.ST_ERR_INVALID
+
+
+def test_library_is_gfx950_only(libpath):
+    # the embedded code-object bundle names its target: amdgcn-amd-amdhsa--gfx950
+    blob = open(libpath, 'rb').read()
+    targets = set(re.findall(rb'amdgcn-amd-amdhsa--(gfx[0-9a-z]+)', blob))
+    assert targets == {b'gfx950'}, targets

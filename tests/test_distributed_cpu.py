@@ -1,0 +1,73 @@
+"""N > 1 orchestration of stein_thinning.distributed on CPU ranks (gloo, world_size 2 and 3):
+row shards + per-step all-gather of candidate records give exactly the single-process indices,
+including exact ties across shard boundaries (lowest global index wins)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from oracle import stein_numpy as o
+from stein_thinning.distributed import run_sharded, shard_bounds
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _data(gf):
+    rng = np.random.default_rng(11)
+    n, d = 1501, 3
+    x = rng.normal(size=(n, d))
+    x[900:1000] = x[100:200]          # duplicates living in different shards
+    g = -x + 0.05 * rng.normal(size=(n, d))
+    g[900:1000] = g[100:200]
+    if gf:
+        log_p = -0.5 * np.sum(x * x, axis=1)
+        log_q = -0.4 * np.sum(x * x, axis=1)
+        return x, g, log_p, log_q
+    return x, g, None, None
+
+
+def _worker(rank, world, port, gf, m, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from tests.cpu_shard_backend import CpuShardBackend
+        x, g, log_p, log_q = _data(gf)
+        s, gs = o._validate_and_standardize(x, g, True)
+        w = np.exp(o._log_weights(log_p, log_q, None)) if gf else None
+        linv = o.make_precon(s, 'med')
+        r0, r1 = shard_bounds(s.shape[0], rank, world)
+        be = CpuShardBackend(s, gs, w, linv[0, 0], np.trace(linv), r0, r1, world, m)
+        idx = run_sharded(be, m)
+        np.save(os.path.join(out_dir, f'idx{rank}.npy'), idx)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,gf', [(2, False), (2, True), (3, False)])
+def test_sharded_equals_single_process(tmp_path, world, gf):
+    m = 40
+    mp.spawn(_worker, args=(world, _free_port(), gf, m, str(tmp_path)), nprocs=world, join=True)
+    x, g, log_p, log_q = _data(gf)
+    want = o.thin_gf(x, log_p, log_q, g, m, preconditioner='med') if gf else o.thin(x, g, m, preconditioner='med')
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}.npy'), want)
+
+
+def test_shard_bounds_cover_rows():
+    for n in [1, 7, 100, 2_000_001]:
+        for world in [1, 2, 3, 8]:
+            if world > n:
+                continue
+            b = [shard_bounds(n, r, world) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            sizes = [e - s for s, e in b]
+            assert max(sizes) - min(sizes) <= 1

@@ -1,0 +1,288 @@
+"""HIP path vs the oracle (run on an MI355X: ``pytest -m gpu``).
+
+Bar: selected indices identical to the NumPy oracle (itself pinned to the reference's golden
+outputs); running sums / pair values bit-identical to the C bit model (oracle/stein_ref.c); KSD within
+1e-10 relative of the NumPy oracle (north_star tolerance 1e-6).
+"""
+import warnings
+
+import numpy as np
+import pytest
+from scipy.stats import multivariate_normal as mvn
+
+from oracle import models
+from oracle import stein_numpy as o
+from tests import oracle_c
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+if not torch.cuda.is_available():
+    pytest.skip('no HIP device', allow_module_level=True)
+
+from stein_thinning import stein as ss  # noqa: E402
+from stein_thinning import thinning as st  # noqa: E402
+from stein_thinning.device import DeviceProblem  # noqa: E402
+from stein_thinning.distributed import HipShardBackend, shard_bounds  # noqa: E402
+
+
+def _native_loaded():
+    from stein_thinning import _native
+    assert _native._LIB is not None
+
+
+# ------------------------------------------------------------------------------------------
+# golden vectors (F1, F2, F3) through the shim
+# ------------------------------------------------------------------------------------------
+def test_f1_golden_indices(golden):
+    sample, gradient, log_p, _, _ = models.bivariate_reference_sample(1000)
+    idx = st.thin(sample, gradient, 20)
+    assert idx.dtype == np.uint32
+    np.testing.assert_array_equal(idx, golden['F1a_thin_bivariate_m20']['indices'])
+    np.testing.assert_array_equal(st.thin_gf(sample, log_p, log_p, gradient, 20), idx)
+    log_q, gq, _, _ = models.gaussian_proxy(sample, ddof=2)
+    np.testing.assert_array_equal(st.thin_gf(sample, log_p, log_q, gq, 20),
+                                  golden['F1c_thin_gf_simple_gaussian_ddof2']['indices'])
+    _native_loaded()
+
+
+@pytest.fixture(scope='module')
+def gm_gpu(gm):
+    sample, sample2, logpdf, score = gm
+    gradient = score(sample)
+    log_p = logpdf(sample)
+    log_q, gq, _, _ = models.gaussian_proxy(sample, ddof=1)
+    return dict(sample=sample, gradient=gradient, log_p=log_p, log_q=log_q, gq=gq,
+                idx_st=st.thin(sample, gradient, 1000, preconditioner='med'),
+                idx_gf=st.thin_gf(sample, log_p, log_q, gq, 1000, preconditioner='med'))
+
+
+def test_f2_gaussian_mixture_1000_steps(gm_gpu, golden):
+    f = golden['F2_gaussian_mixture']
+    s = gm_gpu
+    np.testing.assert_array_equal(s['idx_st'], o.thin(s['sample'], s['gradient'], 1000, preconditioner='med'))
+    np.testing.assert_array_equal(
+        s['idx_gf'], o.thin_gf(s['sample'], s['log_p'], s['log_q'], s['gq'], 1000, preconditioner='med'))
+    assert len(np.unique(s['idx_st'])) == f['unique_counts']['stein']
+    assert len(np.unique(s['idx_gf'])) == f['unique_counts']['gf_simple_gaussian']
+
+
+def test_f2_laplace_collapse(gm, golden):
+    sample, _, logpdf, _ = gm
+    f = golden['F2_gaussian_mixture']
+    lm, lc = np.array(f['laplace_mean']), np.array(f['laplace_cov'])
+    log_p = logpdf(sample)
+    log_q = mvn.logpdf(sample, mean=lm, cov=lc)
+    gq = -np.einsum('ij,kj->ki', np.linalg.inv(lc), sample - lm)
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        idx = st.thin_gf(sample, log_p, log_q, gq, 10_000, preconditioner='med')
+    assert any('log_q differs from log_p by more than 10' in str(x.message) for x in w)
+    assert idx.shape == (10_000,) and set(np.unique(idx).tolist()) == {f['laplace_all_selected']}
+
+
+def test_f3_ksd_curves_on_gpu(gm_gpu, curves):
+    """calculate_ksd (code/src/utils/ksd.py:19-27) through the shim: the reindexed closure runs on
+    the tiled HIP KSD kernel; compare with the oracle and with the report's figure."""
+    def reindex_integrand(integrand, indices):
+        def res(ind1, ind2):
+            return integrand(indices[ind1], indices[ind2])
+        return res
+
+    for name, idx in [('stein', gm_gpu['idx_st']), ('gf_simple_gaussian', gm_gpu['idx_gf'])]:
+        integrand = st._make_stein_integrand(gm_gpu['sample'], gm_gpu['gradient'])
+        ks = ss.ksd(reindex_integrand(integrand, idx), idx.shape[0])
+        want = o.calculate_ksd(gm_gpu['sample'], gm_gpu['gradient'], idx)
+        np.testing.assert_allclose(ks, want, rtol=1e-10)
+        c = np.array(curves['ksd/' + name])
+        np.testing.assert_allclose(ks[c[:, 0].astype(int) - 1], c[:, 1], rtol=1e-7)
+
+
+def test_f4_kmat_on_gpu(gm, golden):
+    sample, _, _, _ = gm
+    f = golden['F2_gaussian_mixture']
+    lm, lc = np.array(f['laplace_mean']), np.array(f['laplace_cov'])
+    gq = -np.einsum('ij,kj->ki', np.linalg.inv(lc), sample - lm)
+    km = ss.kmat(st._make_stein_integrand(sample, gq), sample.shape[0])
+    want = o.kmat(o._make_stein_integrand(sample, gq), sample.shape[0])
+    np.testing.assert_allclose(km, want, rtol=1e-13, atol=1e-13 * np.abs(want).max())
+    assert np.array_equal(km, km.T)
+    assert np.abs(km[np.triu_indices_from(km)]).max() == pytest.approx(f['kmat_laplace_abs_max'], rel=1e-7)
+
+
+# ------------------------------------------------------------------------------------------
+# bit-exactness against the C bit model
+# ------------------------------------------------------------------------------------------
+def _rw_chain(n, d, seed, dup_every=3):
+    """Seeded synthetic chain with many duplicated rows (RW-MH style rejections)."""
+    rng = np.random.default_rng(seed)
+    x = np.cumsum(rng.normal(scale=0.3, size=(n, d)), axis=0) * 0.05 + rng.normal(size=(n, d))
+    rep = rng.random(n) < (1 - 1 / dup_every)
+    for i in range(1, n):
+        if rep[i]:
+            x[i] = x[i - 1]
+    g = -x * np.linspace(0.5, 2.0, d)
+    return x, g
+
+
+@pytest.mark.parametrize('d', [1, 2, 3, 4, 5, 7, 8, 9, 16, 50])
+@pytest.mark.parametrize('gf', [False, True])
+def test_running_sums_bit_exact_vs_c_model(d, gf):
+    n, m = 4099, 25      # odd n: exercises the padded lane pair
+    x, g = _rw_chain(n, d, seed=d)
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    w = None
+    if gf:
+        lw = -0.1 * np.sum(x * x, axis=1)
+        w = np.exp(lw - lw.min())
+    prob = DeviceProblem(s, gs, w, l, tr)
+    idx, A = prob.greedy(m, return_sums=True)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    np.testing.assert_array_equal(idx, cidx)
+    assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
+
+
+@pytest.mark.parametrize('d', [2, 4, 9, 50])
+def test_pair_values_bit_exact_vs_c_model(d):
+    x, g = _rw_chain(700, d, seed=100 + d)
+    s, gs = o._validate_and_standardize(x, g, True)
+    rng = np.random.default_rng(d)
+    w = np.exp(rng.normal(size=700))
+    integ = st.SteinIntegrand(s, gs, o.make_precon(s, 'med'), w)
+    i1 = rng.integers(0, 700, size=5000)
+    i2 = rng.integers(0, 700, size=5000)
+    got = integ(i1, i2)
+    want = oracle_c.pairs(s, gs, w, integ.linv_scale, integ.linv_trace, i1, i2)
+    assert np.array_equal(got, want)
+    # integrand protocol forms used by the reference: (slice, slice), (slice, [j])
+    np.testing.assert_array_equal(integ(slice(None), [5]), oracle_c.pairs(
+        s, gs, w, integ.linv_scale, integ.linv_trace, np.arange(700), np.full(700, 5)))
+    # and against the NumPy oracle integrand (different pow rounding: <= 1e-15 relative)
+    ref = o._make_stein_gf_integrand(x, np.zeros(700), np.log(w), g, preconditioner='med')
+    np.testing.assert_allclose(integ(slice(None), slice(None)), ref(slice(None), slice(None)), rtol=1e-14)
+
+
+def test_vfk0_imq_on_gpu():
+    from stein_thinning import kernel as sk
+    x, g = _rw_chain(300, 4, seed=5)
+    linv = o.make_precon(x, 'med')
+    np.testing.assert_allclose(sk.vfk0_imq(x, x[[7]], g, g[[7]], linv), o.vfk0_imq(x, x[[7]], g, g[[7]], linv),
+                               rtol=1e-14)
+    np.testing.assert_allclose(sk.vfk0_imq(x, x, g, g, linv), o.vfk0_imq(x, x, g, g, linv), rtol=1e-15)
+
+
+# ------------------------------------------------------------------------------------------
+# edge cases the reference allows
+# ------------------------------------------------------------------------------------------
+def test_single_row_and_m_greater_than_n():
+    x = np.array([[0.3, -1.2]])
+    g = -x
+    np.testing.assert_array_equal(st.thin(x, g, 5, standardize=False), np.zeros(5, dtype=np.uint32))
+    x, g = _rw_chain(7, 2, seed=1, dup_every=100)
+    np.testing.assert_array_equal(st.thin(x, g, 30), o.thin(x, g, 30))
+
+
+def test_overflowing_weights_nan_semantics():
+    """exp overflow -> inf/NaN running sums: np.argmin picks the first NaN; the kernel must too."""
+    x, g = _rw_chain(600, 3, seed=9, dup_every=100)
+    log_p = np.zeros(600)
+    log_q = np.linspace(0, 900, 600)       # exp(900) = inf
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        want = o.thin_gf(x, log_p, log_q, g, 12)
+        got = st.thin_gf(x, log_p, log_q, g, 12)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_range_cap_matches_oracle():
+    x, g = _rw_chain(2000, 4, seed=3)
+    log_p = -0.5 * np.sum(x * x, axis=1) * 40
+    log_q = -0.5 * np.sum(x * x, axis=1)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        np.testing.assert_array_equal(st.thin_gf(x, log_p, log_q, g, 50, range_cap=20, preconditioner='med'),
+                                      o.thin_gf(x, log_p, log_q, g, 50, range_cap=20, preconditioner='med'))
+
+
+# ------------------------------------------------------------------------------------------
+# BASELINE configs (sizes the oracle finishes in seconds) and full-size properties
+# ------------------------------------------------------------------------------------------
+def _lv_surrogate(n, seed):
+    from bench import lv_surrogate
+    return lv_surrogate(n, seed)
+
+
+def test_config2_langevin_n2e5_m100():
+    x, g, _, _ = _lv_surrogate(200_000, 12347)
+    np.testing.assert_array_equal(st.thin(x, g, 100, preconditioner='med'),
+                                  o.thin(x, g, 100, preconditioner='med'))
+
+
+def test_config3_gradient_free_n2e5_m100():
+    x, g, log_p, log_q_gq = _lv_surrogate(200_000, 12348)
+    log_q, gq = log_q_gq
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        np.testing.assert_array_equal(st.thin_gf(x, log_p, log_q, gq, 100, preconditioner='med'),
+                                      o.thin_gf(x, log_p, log_q, gq, 100, preconditioner='med'))
+
+
+def test_config5_d50_prefix():
+    from bench import gaussian_d50
+    x, log_p, log_q, gq = gaussian_d50(50_000, 12349)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        np.testing.assert_array_equal(st.thin_gf(x, log_p, log_q, gq, 40, preconditioner='med'),
+                                      o.thin_gf(x, log_p, log_q, gq, 40, preconditioner='med'))
+
+
+def test_config4_full_size_properties():
+    """n = 2e6, m = 1000 (the headline workload): the 20-step prefix equals the oracle, and the final
+    running sums equal diag + 2 sum_t k(., x_idx[t]) bit for bit on sampled rows; the last index is
+    the argmin of the final sums."""
+    n, m = 2_000_000, 1000
+    x, g, _, _ = _lv_surrogate(n, 12345)
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    prob = DeviceProblem(s, gs, None, l, tr)
+    idx20 = prob.greedy(20)
+    np.testing.assert_array_equal(idx20, o.thin(x, g, 20, preconditioner='med'))
+    idx, A = prob.greedy(m, return_sums=True)
+    np.testing.assert_array_equal(idx[:20], idx20)
+    assert idx.max() < n
+    assert int(np.argmin(A)) == int(idx[-1]) or A[int(np.argmin(A))] == A[int(idx[-1])]
+    rows = np.unique(np.concatenate([np.random.default_rng(0).integers(0, n, 1500), idx[-5:].astype(np.int64)]))
+    xs, gss = s[rows], gs[rows]
+    ar = np.arange(rows.shape[0])
+    acc = oracle_c.pairs(xs, gss, None, l, tr, ar, ar)
+    for t in range(m - 1):
+        j = int(idx[t])
+        xx = np.vstack([xs, s[j][None]])
+        gg = np.vstack([gss, gs[j][None]])
+        acc = acc + 2.0 * oracle_c.pairs(xx, gg, None, l, tr, ar, np.full(ar.shape[0], ar.shape[0]))
+    assert np.array_equal(A[rows], acc)
+
+
+def test_two_shards_on_one_gpu_equal_single():
+    """HipShardBackend with nranks = 2 in one process (records exchanged by torch.cat in place of
+    RCCL) reproduces the single-device indices, including ties across the shard boundary."""
+    x, g = _rw_chain(30_001, 4, seed=21)
+    x[20_000:20_500] = x[1_000:1_500]
+    g[20_000:20_500] = g[1_000:1_500]
+    m = 60
+    integ = st._make_stein_integrand(x, g, preconditioner='med')
+    want = integ.device_problem().greedy(m)
+    bes = [HipShardBackend(integ, *shard_bounds(integ.n, r, 2), 2, m) for r in range(2)]
+    for t in range(m):
+        for be in bes:
+            be.step(t)
+        allrec = torch.cat([be.send for be in bes])
+        for be in bes:
+            be.recv.copy_(allrec)
+    for be in bes:
+        be.finalize(m - 1)
+        np.testing.assert_array_equal(be.indices(), want)
+    np.testing.assert_array_equal(want, o.thin(x, g, m, preconditioner='med'))

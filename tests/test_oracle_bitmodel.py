@@ -1,0 +1,117 @@
+"""The C bit model (oracle/stein_ref.c) restates NumPy's evaluation order of the reference vfk0_imq.
+
+(1) a scalar Python model with NumPy's own power() reproduces oracle.vfk0_imq bit for bit
+    (sequential sums for qf/t1/t2, NumPy pairwise_sum for t3) at d = 1, 2, 4, 9, 50;
+(2) the C model equals that scalar model with correctly rounded powers, bit for bit;
+(3) C-model greedy indices equal the NumPy oracle's on seeded inputs.
+"""
+import decimal
+
+import numpy as np
+import pytest
+
+from oracle import stein_numpy as o
+from tests import oracle_c
+
+decimal.getcontext().prec = 80
+
+
+def _seq(v):
+    acc = v[0]
+    for x in v[1:]:
+        acc = acc + x
+    return acc
+
+
+def _pairwise(v):
+    n = len(v)
+    if n < 8:
+        r = np.float64(0.0)
+        for x in v:
+            r = r + x
+        return r
+    r = list(v[:8])
+    i = 8
+    while i < n - (n % 8):
+        for j in range(8):
+            r[j] = r[j] + v[i + j]
+        i += 8
+    res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]))
+    while i < n:
+        res = res + v[i]
+        i += 1
+    return res
+
+
+def _cr_pow(q, e):
+    d = decimal.Decimal(float(q))
+    v = d * d.sqrt() if e == 1.5 else d * d * d.sqrt()
+    return np.float64(float(v))
+
+
+def _model(xi, xj, gi, gj, l, tr, powf):
+    l2 = l * l
+    dl = xi - xj
+    gd = gi - gj
+    qf = np.float64(1.0) + _seq((l * dl) * dl)
+    t1 = (-3 * _seq((l2 * dl) * dl)) / powf(qf, 2.5)
+    t2 = (tr + _seq((l * gd) * dl)) / powf(qf, 1.5)
+    t3 = _pairwise(gi * gj) / np.sqrt(qf)
+    return (t1 + t2) + t3
+
+
+def _problem(d, n=150, seed=0):
+    rng = np.random.default_rng(seed + d)
+    x = rng.normal(size=(n, d)) * rng.uniform(0.2, 3, size=d)
+    g = rng.normal(size=(n, d)) * 2
+    return x, g
+
+
+@pytest.mark.parametrize('d', [1, 2, 4, 9, 50])
+@pytest.mark.parametrize('pre', ['id', 'med'])
+def test_scalar_model_matches_numpy_oracle(d, pre):
+    x, g = _problem(d)
+    linv = o.make_precon(x, pre)
+    l, tr = linv[0, 0], np.trace(linv)
+    j = 3
+    ref = o.vfk0_imq(x, x[[j]], g, g[[j]], linv)
+    got = np.array([_model(x[i], x[j], g[i], g[j], l, tr, np.power) for i in range(x.shape[0])])
+    np.testing.assert_array_equal(got, ref)
+    refd = o.vfk0_imq(x, x, g, g, linv)
+    gotd = np.array([_model(x[i], x[i], g[i], g[i], l, tr, np.power) for i in range(x.shape[0])])
+    np.testing.assert_array_equal(gotd, refd)
+
+
+@pytest.mark.parametrize('d', [1, 2, 4, 9, 50])
+def test_c_model_is_scalar_model_with_correct_rounding(d):
+    x, g = _problem(d, n=60)
+    linv = o.make_precon(x, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    i1 = np.arange(60)
+    i2 = np.full(60, 5)
+    got = oracle_c.pairs(x, g, None, l, tr, i1, i2)
+    want = np.array([_model(x[i], x[5], g[i], g[5], l, tr, _cr_pow) for i in i1])
+    np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize('d,pre,gf', [(2, 'id', False), (4, 'med', False), (4, 'med', True), (9, 'id', True)])
+def test_c_model_greedy_matches_numpy_oracle(d, pre, gf):
+    rng = np.random.default_rng(7)
+    n, m = 3000, 60
+    x = rng.normal(size=(n, d))
+    x[1000:1300] = x[:300]          # duplicated rows: exact ties, lowest index wins
+    g = -x + 0.1 * rng.normal(size=(n, d))
+    g[1000:1300] = g[:300]
+    if gf:
+        log_p = -0.5 * np.sum(x * x, axis=1)
+        log_q = -0.45 * np.sum(x * x, axis=1)
+        want = o.thin_gf(x, log_p, log_q, g, m, preconditioner=pre)
+        s, gs = o._validate_and_standardize(x, g, True)
+        w = np.exp(o._log_weights(log_p, log_q, None))
+    else:
+        want = o.thin(x, g, m, preconditioner=pre)
+        s, gs = o._validate_and_standardize(x, g, True)
+        w = None
+    linv = o.make_precon(s, pre)
+    idx, _ = oracle_c.greedy(s, gs, w, linv[0, 0], np.trace(linv), m)
+    np.testing.assert_array_equal(idx, want)

@@ -1,0 +1,143 @@
+"""Host-side logic of the stein_thinning shim (no GPU): validation, standardisation, preconditioner,
+log-weights, the integrand protocol loops, and that the device path refuses to run without HIP."""
+import subprocess
+import sys
+import warnings
+
+import numpy as np
+import pytest
+
+from oracle import models
+from oracle import stein_numpy as o
+from stein_thinning import kernel as sk
+from stein_thinning import stein as ss
+from stein_thinning import thinning as st
+
+
+@pytest.fixture(scope='module')
+def biv():
+    return models.bivariate_reference_sample(1000)
+
+
+def test_standardize_bit_identical_to_oracle(biv):
+    sample, gradient, _, _, _ = biv
+    s1, g1 = st._validate_and_standardize(sample, gradient, True)
+    s2, g2 = o._validate_and_standardize(sample, gradient, True)
+    assert np.array_equal(s1, s2) and np.array_equal(g1, g2)
+    s3, g3 = st._validate_and_standardize(sample, gradient, False)
+    assert np.array_equal(s3, sample) and np.array_equal(g3, gradient)
+
+
+@pytest.mark.parametrize('pre', ['id', 'med', 'sclmed', 2.5, '0.5'])
+def test_precon_bit_identical_to_oracle(biv, pre):
+    s, _ = o._validate_and_standardize(biv[0], biv[1], True)
+    assert np.array_equal(sk.make_precon(s, pre), o.make_precon(s, pre))
+
+
+def test_precon_med_subsamples_large_n():
+    rng = np.random.default_rng(0)
+    x = rng.normal(size=(5000, 3))
+    assert np.array_equal(sk.make_precon(x, 'med'), o.make_precon(x, 'med'))
+
+
+def test_precon_errors():
+    x = np.ones((10, 2))
+    with pytest.raises(ValueError):
+        sk.make_precon(x, 'med')
+    with pytest.raises(ValueError):
+        sk.make_precon(x, 'bogus')
+
+
+@pytest.mark.parametrize('bad', [
+    (np.zeros(5), np.zeros(5)),                       # not 2-D
+    (np.zeros((0, 2)), np.zeros((0, 2))),             # empty
+    (np.zeros((5, 2)), np.zeros((5, 3))),             # inconsistent
+    (np.array([[np.nan, 1.], [2., 3.]]), np.ones((2, 2))),
+    (np.array([[np.inf, 1.], [2., 3.]]), np.ones((2, 2))),
+    (np.ones((4, 2)), np.ones((4, 2))),               # zero scale
+])
+def test_validation_errors(bad):
+    with pytest.raises(ValueError):
+        st._validate_and_standardize(bad[0], bad[1], True)
+
+
+def test_log_weights_warning_and_anchor():
+    log_p = np.array([0., -1., -30.])
+    log_q = np.array([0., 0., 0.])
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter('always')
+        lw = st._log_weights(log_p, log_q, None)
+    assert any('log_q differs from log_p by more than 10' in str(x.message) for x in w)
+    assert np.array_equal(lw, o._log_weights(log_p, log_q, None))
+    assert lw.min() == 0
+    assert np.array_equal(st._log_weights(log_p, log_q, 5.0), np.minimum(lw, 5.0))
+    with warnings.catch_warnings():
+        warnings.simplefilter('error')
+        st._log_weights(np.zeros(3), np.array([0., 1., 2.]), None)
+
+
+def test_protocol_greedy_with_user_integrand_matches_oracle(biv):
+    sample, gradient, _, _, _ = biv
+    integrand = o._make_stein_integrand(sample, gradient)    # a plain NumPy callable (user plug-in)
+    np.testing.assert_array_equal(st._greedy_search(20, integrand), o._greedy_search(20, integrand))
+
+
+def test_greedy_argument_errors():
+    with pytest.raises(IndexError):
+        st._greedy_search(0, lambda a, b: np.zeros(3))
+    with pytest.raises(ValueError):
+        st._greedy_search(-1, lambda a, b: np.zeros(3))
+
+
+def test_reference_test_ksd_through_shim(golden):
+    """code/tests/test_ksd.py verbatim semantics, run against the shim's kmat."""
+    f = golden['F5_test_ksd']
+    mat = np.array(f['mat'])
+
+    def integrand(ind1, ind2):
+        return mat[ind1, ind2]
+
+    def reindex_integrand(integrand, indices):   # code/src/utils/ksd.py:9-16
+        def res(ind1, ind2):
+            return integrand(indices[ind1], indices[ind2])
+        return res
+    res = ss.kmat(reindex_integrand(integrand, np.array(f['indices'])), mat.shape[0])
+    np.testing.assert_array_equal(res, f['expected'])
+
+
+def test_protocol_ksd_with_user_integrand_matches_oracle(biv):
+    sample, gradient, _, _, _ = biv
+    integrand = o._make_stein_integrand(sample[:200], gradient[:200])
+    np.testing.assert_allclose(ss.ksd(integrand, 50), o.ksd(integrand, 50), rtol=1e-12)
+
+
+def test_reindex_closure_is_recognised():
+    s = np.random.default_rng(0).normal(size=(20, 2))
+    integ = st.SteinIntegrand(s, -s, np.identity(2))
+    idx = np.array([3, 1, 2])
+
+    def reindex_integrand(integrand, indices):   # code/src/utils/ksd.py:9-16
+        def res(ind1, ind2):
+            return integrand(indices[ind1], indices[ind2])
+        return res
+    got = ss._resolve(reindex_integrand(integ, idx))
+    assert got is not None and got[0] is integ and np.array_equal(got[1], idx)
+    assert ss._resolve(lambda a, b: a) is None
+
+
+def test_device_path_refuses_without_gpu(biv):
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip('GPU present')
+    from stein_thinning import _native
+    with pytest.raises(_native.HipExtensionError):
+        st.thin(biv[0], biv[1], 5)
+
+
+def test_import_touches_no_gpu():
+    code = ('import sys; sys.path.insert(0, "gradient-free-mcmc-postprocessing_amd"); '
+            'import stein_thinning, stein_thinning.thinning, stein_thinning.stein, stein_thinning.kernel; '
+            'assert "torch" not in sys.modules, "torch imported at package import"')
+    import os
+    subprocess.run([sys.executable, '-c', code], check=True,
+                   cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
