@@ -142,27 +142,24 @@ def cpu_baseline(cfg, integrand, steps: int):
 
 
 def kernel_timing(prob, n_points: int, repeats: int = 3):
-    """Average duration of the fused step kernel, measured with HIP events on the launch stream."""
+    """Average duration of the fused step kernel, measured with HIP events around single step
+    launches (st_greedy_steps) on the stream they are launched on."""
     import torch
     from stein_thinning import _native as nat
     L = nat.lib()
     idx, a, ws = prob.greedy_buffers(n_points)
-    stride = int(L.st_candidate_stride(prob.d))
-    cands = torch.zeros(2 * stride, dtype=torch.float64, device=prob.x.device)
     stream = torch.cuda.current_stream()
     durs = []
     for _ in range(repeats):
         evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_points)]
         for t in range(n_points):
-            cin = cands[((t + 1) & 1) * stride:]
-            cout = cands[(t & 1) * stride:]
             evs[t][0].record(stream)
-            nat.check(L.st_greedy_step(nat.ptr(prob.x), nat.ptr(prob.g), nat.ptr(prob.w), prob.n, prob.d, prob.ld,
-                                       prob.l, prob.tr, 0, t, 1, nat.ptr(cin), nat.ptr(cout), nat.ptr(idx),
-                                       nat.ptr(a), nat.ptr(ws), ws.numel() * 8, nat.stream_handle()), 'step')
+            nat.check(L.st_greedy_steps(nat.ptr(prob.x), nat.ptr(prob.g), nat.ptr(prob.w), prob.n, prob.d, prob.ld,
+                                        prob.l, prob.tr, t, t + 1, n_points, nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
+                                        ws.numel() * 8, nat.stream_handle()), 'st_greedy_steps')
             evs[t][1].record(stream)
         torch.cuda.synchronize()
-        durs.extend(e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs[1:])   # t >= 1: streaming steps
+        durs.extend(e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs[1:-1])   # streaming steps only
     return float(np.mean(durs)), float(np.median(durs))
 
 

@@ -33,46 +33,28 @@ int check_problem(const double* x, const double* g, const double* w, int64_t n, 
     if (d < 1) return fail(ST_ERR_INVALID, "d must be >= 1 (got %d)", d);
     if (d > st::kMaxDim)
         return fail(ST_ERR_UNSUPPORTED, "d = %d exceeds the supported maximum %d", d, st::kMaxDim);
-    if (ld < n + (n & 1) || (ld & 1))
-        return fail(ST_ERR_INVALID, "ld must be even and >= n + (n & 1) (n=%lld, ld=%lld)",
+    if (ld < n || (ld & 7))
+        return fail(ST_ERR_INVALID, "ld must be a multiple of 8 and >= n (n=%lld, ld=%lld)",
                     (long long)n, (long long)ld);
     if (!aligned16(x) || !aligned16(g) || (w && !aligned16(w)))
         return fail(ST_ERR_INVALID, "device arrays must be 16-byte aligned");
     return ST_OK;
 }
 
-// workspace layout: [ticket: 16 B][part_val: kMaxBlocks f64][part_idx: kMaxBlocks i64][cands: 2 x stride f64]
-struct GreedyWs {
-    unsigned* ticket;
-    double* part_val;
-    int64_t* part_idx;
-    double* cands;
-};
+// workspace layout: two ping-pong banks of per-block candidate records, kMaxBlocks x stride each
+int64_t greedy_ws_bytes(int32_t d) { return 2 * (int64_t)st::kMaxBlocks * st::cand_stride(d) * 8; }
 
-int64_t greedy_ws_bytes(int32_t d) {
-    return 16 + (int64_t)st::kMaxBlocks * 16 + 2 * st::cand_stride(d) * 8;
-}
-
-GreedyWs carve(void* ws, int32_t d) {
-    char* p = static_cast<char*>(ws);
-    GreedyWs w;
-    w.ticket = reinterpret_cast<unsigned*>(p);
-    w.part_val = reinterpret_cast<double*>(p + 16);
-    w.part_idx = reinterpret_cast<int64_t*>(p + 16 + (int64_t)st::kMaxBlocks * 8);
-    w.cands = reinterpret_cast<double*>(p + 16 + (int64_t)st::kMaxBlocks * 16);
-    (void)d;
-    return w;
+double* bank(void* ws, int32_t d, int b) {
+    return static_cast<double*>(ws) + (int64_t)b * st::kMaxBlocks * st::cand_stride(d);
 }
 
 st::GreedyArgs make_args(const double* x, const double* g, const double* w, int64_t n, int32_t d,
-                         int64_t ld, double l, double tr, double* A, const GreedyWs& ws) {
+                         int64_t ld, double l, double tr, double* A) {
     st::GreedyArgs a{};
     a.x = x; a.g = g; a.w = w; a.A = A;
     a.n = n; a.ld = ld; a.d = d; a.l = l; a.tr = tr;
     a.row_offset = 0;
-    a.nranks = 1;
-    a.cand_stride = st::cand_stride(d);
-    a.part_val = ws.part_val; a.part_idx = ws.part_idx; a.ticket = ws.ticket;
+    a.rec_stride = st::cand_stride(d);
     return a;
 }
 
@@ -90,18 +72,25 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks) {
     return greedy_ws_bytes(d);
 }
 
+int st_tune(int32_t key, int32_t value) {
+    if (st::tune(key, value) != 0) return fail(ST_ERR_INVALID, "bad tuning key/value %d=%d", key, value);
+    return ST_OK;
+}
+
 int64_t st_candidate_stride(int32_t d) {
     if (d < 1 || d > st::kMaxDim) return -1;
     return st::cand_stride(d);
 }
 
-int st_greedy(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
-              int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t n_points,
-              uint32_t* idx_out, double* a_work, void* workspace, int64_t workspace_bytes,
-              void* stream) {
+int st_greedy_steps(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
+                    int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t t_begin,
+                    int64_t t_end, int64_t n_points, uint32_t* idx_out, double* a_work,
+                    void* workspace, int64_t workspace_bytes, void* stream) {
     int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
     if (rc) return rc;
     if (n_points < 1) return fail(ST_ERR_INVALID, "n_points must be >= 1");
+    if (t_begin < 0 || t_end < t_begin || t_end > n_points)
+        return fail(ST_ERR_INVALID, "need 0 <= t_begin <= t_end <= n_points");
     if (!idx_out || !a_work || !workspace) return fail(ST_ERR_INVALID, "NULL output/workspace");
     if (!aligned16(a_work) || !aligned16(workspace))
         return fail(ST_ERR_INVALID, "a_work/workspace must be 16-byte aligned");
@@ -109,22 +98,30 @@ int st_greedy(const double* x_soa, const double* g_soa, const double* weights, i
         return fail(ST_ERR_INVALID, "workspace too small (%lld < %lld)", (long long)workspace_bytes,
                     (long long)greedy_ws_bytes(d));
     hipStream_t s = static_cast<hipStream_t>(stream);
-    GreedyWs ws = carve(workspace, d);
-    rc = hip_check(hipMemsetAsync(ws.ticket, 0, 16, s), "hipMemsetAsync(ticket)");
-    if (rc) return rc;
-    st::GreedyArgs a = make_args(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, a_work, ws);
+    st::GreedyArgs a = make_args(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, a_work);
     a.idx_out = idx_out;
-    const int64_t stride = a.cand_stride;
-    for (int64_t t = 0; t < n_points; ++t) {
+    const int blocks = st::greedy_blocks(n, d);
+    for (int64_t t = t_begin; t < t_end; ++t) {
         a.t = t;
-        a.cands_in = ws.cands + ((t + 1) & 1) * stride;
-        a.cand_out = ws.cands + (t & 1) * stride;
-        rc = hip_check(st::launch_greedy_step(a, t == 0, s), "greedy step launch");
+        a.recs_in = bank(workspace, d, (int)((t + 1) & 1));
+        a.nrecs_in = blocks;
+        a.recs_out = bank(workspace, d, (int)(t & 1));
+        rc = hip_check(st::launch_greedy_step(a, t == 0, blocks, s), "greedy step launch");
         if (rc) return rc;
     }
-    return hip_check(st::launch_greedy_finalize(ws.cands + ((n_points - 1) & 1) * stride, 1,
-                                                stride, idx_out, n_points - 1, s),
+    if (t_end < n_points || t_end == t_begin) return ST_OK;
+    return hip_check(st::launch_greedy_finalize(bank(workspace, d, (int)((n_points - 1) & 1)), blocks,
+                                                a.rec_stride, idx_out, n_points - 1, s),
                      "greedy finalize launch");
+}
+
+int st_greedy(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
+              int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t n_points,
+              uint32_t* idx_out, double* a_work, void* workspace, int64_t workspace_bytes,
+              void* stream) {
+    if (n_points < 1) return fail(ST_ERR_INVALID, "n_points must be >= 1");
+    return st_greedy_steps(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, 0, n_points,
+                           n_points, idx_out, a_work, workspace, workspace_bytes, stream);
 }
 
 int st_greedy_step(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
@@ -144,19 +141,18 @@ int st_greedy_step(const double* x_soa, const double* g_soa, const double* weigh
         return fail(ST_ERR_INVALID, "a_work/workspace must be 16-byte aligned");
     if (workspace_bytes < greedy_ws_bytes(d)) return fail(ST_ERR_INVALID, "workspace too small");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    GreedyWs ws = carve(workspace, d);
-    if (t == 0) {
-        rc = hip_check(hipMemsetAsync(ws.ticket, 0, 16, s), "hipMemsetAsync(ticket)");
-        if (rc) return rc;
-    }
-    st::GreedyArgs a = make_args(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, a_work, ws);
+    st::GreedyArgs a = make_args(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, a_work);
     a.row_offset = row_offset;
-    a.nranks = nranks;
     a.t = t;
-    a.cands_in = cands_in;
-    a.cand_out = cand_out;
+    a.recs_in = cands_in;
+    a.nrecs_in = nranks;
+    a.recs_out = bank(workspace, d, 0);
     a.idx_out = idx_out;
-    return hip_check(st::launch_greedy_step(a, t == 0, s), "greedy step launch");
+    const int blocks = st::greedy_blocks(n, d);
+    rc = hip_check(st::launch_greedy_step(a, t == 0, blocks, s), "greedy step launch");
+    if (rc) return rc;
+    return hip_check(st::launch_greedy_publish(a.recs_out, blocks, a.rec_stride, d, cand_out, s),
+                     "greedy publish launch");
 }
 
 int st_greedy_finalize(const double* cands_in, int32_t nranks, int32_t d, uint32_t* idx_out,

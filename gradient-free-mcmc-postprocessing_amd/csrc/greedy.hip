@@ -1,21 +1,21 @@
-// Greedy Stein-thinning step kernels for gfx950 (K1 diag, K2 fused step, K3 argmin finalize).
+// Greedy Stein-thinning step kernels for gfx950 (K1 diagonal, K2 fused step, K3 finalize).
 //
 // Replaces the reference's hot loop (stein_thinning.thinning._greedy_search, restated at
 // JAX_Stein_Thinning.ipynb cell 22, json ~281-295; Algorithm 3, report.tex:413-426):
 //     A = integrand(:, :); idx[0] = argmin(A)
 //     for t in 1..m-1:  A += 2 * integrand(:, [idx[t-1]]);  idx[t] = argmin(A)
 //
-// One launch per greedy step.  Every launch:
-//   1. picks the previous step's winner from R rank candidates (lowest value, then lowest global
-//      index; NaN counts as minimum -- np.argmin semantics) and stages its row (x_j, g_j, w_j) in LDS;
-//   2. streams the candidate columns of this rank's shard (SoA, coalesced 16-B loads, two candidates
-//      per lane), evaluates k(x_i, x_j), updates the running sum A_i in place;
-//   3. reduces (A_i, i) to one per-block MINLOC; the last block to arrive (agent-scope ticket)
-//      reduces the block partials and publishes this rank's candidate {val, gidx, x, g, w} for the
-//      next launch (and, for R > 1 ranks, for the RCCL all-gather between launches).
-// Inter-workgroup hand-off follows the measured valid form of MI355X_MICROARCH.md (table row 1):
-// 8-B agent-scope (sc1) stores, every storing wave drained (s_waitcnt vmcnt(0)) before ONE lane's
-// agent-scope atomic add; the last arriver reads with agent-scope (sc1) loads.
+// One launch per greedy step, no inter-workgroup synchronisation inside a launch:
+//   head   -- every block reduces the K candidate records of the previous launch (np.argmin order:
+//             NaN first, then lowest value, then lowest global index) and stages the winner's row
+//             (x_j, g_j, w_j) in LDS; block 0 writes idx[t-1].  For one GPU the K records are the
+//             previous launch's per-block records; for R ranks they are the R rank records the
+//             RCCL all-gather delivered (greedy_publish reduces a rank's block records first).
+//   stream -- the candidate columns of this shard (SoA, coalesced 16-B loads, CPT adjacent
+//             candidates per lane, optional register prefetch of the next tile), k(x_i, x_j),
+//             A_i += 2 k in place; per-lane MINLOC.
+//   tail   -- block MINLOC and ONE record {A_min, global index, x row, g row, w} per block.
+// The kernel boundary is the only hand-off (no tickets, no last-block epilogue).
 #include "stein_math.hpp"
 #include "stein_internal.hpp"
 
@@ -46,161 +46,214 @@ __device__ __forceinline__ void block_minloc(double& v, int64_t& i, double* s_v,
     __syncthreads();
 }
 
-__device__ __forceinline__ void store_agent_f64(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), __double_as_longlong(v), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double load_agent_f64(const double* p) {
-    return __longlong_as_double(__hip_atomic_load(reinterpret_cast<const uint64_t*>(p),
-                                                  __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-}
-__device__ __forceinline__ void store_agent_i64(int64_t* p, int64_t v) {
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), (uint64_t)v, __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int64_t load_agent_i64(const int64_t* p) {
-    return (int64_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(p), __ATOMIC_RELAXED,
-                                      __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ int64_t rec_gidx(const double* r) {
+    return (int64_t)__double_as_longlong(r[1]);
 }
 
-// Select the winner among R candidates (deterministic, identical in every block and rank).
-// Stages the winner row {x[d], g[d], w} in s_row; returns the winner's global index.
-__device__ __forceinline__ int64_t select_winner(const double* __restrict__ cands, int nranks,
-                                                 int d, int64_t stride, double* s_row,
-                                                 int64_t* s_gidx) {
-    if (threadIdx.x < 64) {
-        double v = INFINITY;
-        int64_t gi = INT64_MAX;
-        if ((int)threadIdx.x < nranks) {
-            const double* c = cands + threadIdx.x * stride;
-            v = c[0];
-            gi = (int64_t)__double_as_longlong(c[1]);
-        }
-        wave_minloc(v, gi);
-        if (threadIdx.x == 0) *s_gidx = gi;
-    }
-    __syncthreads();
-    const int64_t gidx = *s_gidx;
-    // which rank slot holds it: the first slot whose gidx matches (gidx unique across ranks)
-    int win = 0;
-    for (int r = 0; r < nranks; ++r)
-        if ((int64_t)__double_as_longlong(cands[r * stride + 1]) == gidx) { win = r; break; }
-    const double* row = cands + win * stride + kCandHeader;
-    for (int k = threadIdx.x; k < 2 * d + 1; k += kBlock) s_row[k] = row[k];
-    __syncthreads();
-    return gidx;
-}
-
-// Last-arriver epilogue: reduce block partials, publish {val, gidx, x_row, g_row, w} of the
-// local best.  Called by every thread of the block that drew the last ticket.
-__device__ void publish_rank_candidate(const GreedyArgs& a, double* s_v, int64_t* s_i) {
+// Head: reduce K records; stage the winner row (2d+1 doubles) in s_row; return its global index.
+// ROWREG (d <= 8): each thread pre-loads the row of its best record with the header (no dependent
+// global round trip); otherwise the winner row is fetched after the reduction.
+template <bool ROWREG, int DR>
+__device__ __forceinline__ int64_t pick_winner(const double* __restrict__ recs, int K,
+                                               int64_t stride, int d, double* s_row,
+                                               double* s_v, int64_t* s_i, int* s_slot) {
     double v = INFINITY;
-    int64_t li = INT64_MAX;
-    for (int b = threadIdx.x; b < (int)gridDim.x; b += kBlock) {
-        const double pv = load_agent_f64(a.part_val + b);
-        const int64_t pi = load_agent_i64(a.part_idx + b);
-        if (better(pv, pi, v, li)) { v = pv; li = pi; }
+    int64_t gi = INT64_MAX;
+    int slot = -1;
+    double row[ROWREG ? 2 * DR + 1 : 1];
+    for (int r = threadIdx.x; r < K; r += kBlock) {
+        const double* rec = recs + (int64_t)r * stride;
+        const double rv = rec[0];
+        const int64_t ri = rec_gidx(rec);
+        double rrow[ROWREG ? 2 * DR + 1 : 1];
+        if constexpr (ROWREG) {
+#pragma unroll
+            for (int k = 0; k < 2 * DR + 1; ++k) rrow[k] = rec[kCandHeader + k];
+        }
+        if (better(rv, ri, v, gi)) {
+            v = rv; gi = ri; slot = r;
+            if constexpr (ROWREG) {
+#pragma unroll
+                for (int k = 0; k < 2 * DR + 1; ++k) row[k] = rrow[k];
+            }
+        }
     }
+    double bv = v;
+    int64_t bi = gi;
+    block_minloc(bv, bi, s_v, s_i);
+    if (slot >= 0 && gi == bi) {   // global indices are unique across records
+        if constexpr (ROWREG) {
+#pragma unroll
+            for (int k = 0; k < 2 * DR + 1; ++k) s_row[k] = row[k];
+        } else {
+            *s_slot = slot;
+        }
+    }
+    __syncthreads();
+    if constexpr (!ROWREG) {
+        const double* rec = recs + (int64_t)(*s_slot) * stride + kCandHeader;
+        for (int k = threadIdx.x; k < 2 * d + 1; k += kBlock) s_row[k] = rec[k];
+        __syncthreads();
+    }
+    return bi;
+}
+
+// Tail: block MINLOC and this block's record.
+__device__ __forceinline__ void write_block_record(const GreedyArgs& a, double v, int64_t li,
+                                                   double* s_v, int64_t* s_i) {
     block_minloc(v, li, s_v, s_i);
-    double* out = a.cand_out;
+    double* out = a.recs_out + (int64_t)blockIdx.x * a.rec_stride;
+    const int d = a.d;
     if (threadIdx.x == 0) {
         out[0] = v;
-        out[1] = __longlong_as_double((long long)(a.row_offset + li));
+        out[1] = __longlong_as_double((long long)(li == INT64_MAX ? INT64_MAX : a.row_offset + li));
     }
-    const int d = a.d;
-    for (int k = threadIdx.x; k < 2 * d + 1; k += kBlock) {
-        double val;
-        if (k < d) val = a.x[(int64_t)k * a.ld + li];
-        else if (k < 2 * d) val = a.g[(int64_t)(k - d) * a.ld + li];
-        else val = a.w ? a.w[li] : 1.0;
-        out[kCandHeader + k] = val;
+    if (li != INT64_MAX) {
+        for (int k = threadIdx.x; k < 2 * d + 1; k += kBlock) {
+            double val;
+            if (k < d) val = a.x[(int64_t)k * a.ld + li];
+            else if (k < 2 * d) val = a.g[(int64_t)(k - d) * a.ld + li];
+            else val = a.w ? a.w[li] : 1.0;
+            out[kCandHeader + k] = val;
+        }
     }
-}
-
-// Per-block partial -> ticket; returns true in every thread of the last-arriving block.
-__device__ __forceinline__ bool arrive(const GreedyArgs& a, double v, int64_t i, int* s_flag) {
-    if (threadIdx.x == 0) {
-        store_agent_f64(a.part_val + blockIdx.x, v);
-        store_agent_i64(a.part_idx + blockIdx.x, i);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const unsigned target = (unsigned)((a.t + 1) * (int64_t)gridDim.x - 1);
-        const unsigned old = __hip_atomic_fetch_add(a.ticket, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = (old == target);
-    }
-    __syncthreads();
-    return *s_flag != 0;
 }
 
 // ------------------------------------------------------------------------------------------
 // K1/K2: compile-time d.  DIAG: A_i = k(x_i, x_i) [w_i^2]; else A_i += 2 k(x_i, x_j) [w_i w_j].
-// Two adjacent candidates per lane (16-B loads of the SoA columns), grid-stride.
+// CPT adjacent candidates per lane (16-B loads of the SoA columns for CPT >= 2), grid-stride;
+// PF: the next tile is loaded into registers before the current one is evaluated.
 // ------------------------------------------------------------------------------------------
-template <int D, bool GF, bool DIAG>
+template <int D, bool GF, bool DIAG, int CPT>
+struct Tile {
+    double x[DIAG ? 1 : D][CPT];
+    double g[D][CPT];
+    double w[GF ? CPT : 1];
+    double a[DIAG ? 1 : CPT];
+};
+
+template <int D, bool GF, bool DIAG, int CPT>
+__device__ __forceinline__ void load_tile(const GreedyArgs& a, int64_t i0, Tile<D, GF, DIAG, CPT>& t) {
+    const int64_t ld = a.ld;
+    if constexpr (CPT == 1) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            if constexpr (!DIAG) t.x[k][0] = a.x[k * ld + i0];
+            t.g[k][0] = a.g[k * ld + i0];
+        }
+        if constexpr (GF) t.w[0] = a.w[i0];
+        if constexpr (!DIAG) t.a[0] = a.A[i0];
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+#pragma unroll
+            for (int c = 0; c < CPT; c += 2) {
+                if constexpr (!DIAG) {
+                    const double2 xv = *reinterpret_cast<const double2*>(a.x + k * ld + i0 + c);
+                    t.x[k][c] = xv.x; t.x[k][c + 1] = xv.y;
+                }
+                const double2 gv = *reinterpret_cast<const double2*>(a.g + k * ld + i0 + c);
+                t.g[k][c] = gv.x; t.g[k][c + 1] = gv.y;
+            }
+        }
+#pragma unroll
+        for (int c = 0; c < CPT; c += 2) {
+            if constexpr (GF) {
+                const double2 wv = *reinterpret_cast<const double2*>(a.w + i0 + c);
+                t.w[c] = wv.x; t.w[c + 1] = wv.y;
+            }
+            if constexpr (!DIAG) {
+                const double2 av = *reinterpret_cast<const double2*>(a.A + i0 + c);
+                t.a[c] = av.x; t.a[c + 1] = av.y;
+            }
+        }
+    }
+}
+
+template <int D, bool GF, bool DIAG, int CPT>
+__device__ __forceinline__ void eval_tile(const GreedyArgs& a, int64_t i0,
+                                          const Tile<D, GF, DIAG, CPT>& t, const double (&xj)[D],
+                                          const double (&gj)[D], double wj, double l, double l2,
+                                          double tr, double& best_v, int64_t& best_i) {
+    double out[CPT];
+#pragma unroll
+    for (int c = 0; c < CPT; ++c) {
+        double gi[D];
+#pragma unroll
+        for (int k = 0; k < D; ++k) gi[k] = t.g[k][c];
+        double kv;
+        if constexpr (DIAG) {
+            kv = diag_value_ct<D>(gi, tr);
+            if constexpr (GF) kv = (kv * t.w[c]) * t.w[c];
+            out[c] = kv;
+        } else {
+            double xi[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) xi[k] = t.x[k][c];
+            kv = pair_value_ct<D>(xi, gi, xj, gj, l, l2, tr);
+            if constexpr (GF) kv = (kv * t.w[c]) * wj;
+            out[c] = t.a[c] + 2.0 * kv;
+        }
+    }
+    if constexpr (CPT == 1) {
+        a.A[i0] = out[0];
+    } else {
+#pragma unroll
+        for (int c = 0; c < CPT; c += 2)
+            *reinterpret_cast<double2*>(a.A + i0 + c) = make_double2(out[c], out[c + 1]);
+    }
+#pragma unroll
+    for (int c = 0; c < CPT; ++c)
+        if (i0 + c < a.n && better(out[c], i0 + c, best_v, best_i)) { best_v = out[c]; best_i = i0 + c; }
+}
+
+template <int D, bool GF, bool DIAG, int CPT, bool PF>
 __global__ __launch_bounds__(kBlock) void greedy_step_ct(GreedyArgs a) {
     __shared__ double s_row[2 * D + 1];
-    __shared__ int64_t s_gidx;
     __shared__ double s_v[kWaves];
     __shared__ int64_t s_i[kWaves];
-    __shared__ int s_flag;
+    __shared__ int s_slot;
+
+    const int64_t nunits = (a.n + CPT - 1) / CPT;
+    const int64_t ustride = (int64_t)gridDim.x * kBlock;
+    int64_t u = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    using T = Tile<D, GF, DIAG, CPT>;
+    T cur;
+    if (PF && u < nunits) load_tile<D, GF, DIAG, CPT>(a, u * CPT, cur);   // in flight during the head
 
     double xj[D], gj[D];
     double wj = 1.0;
     if constexpr (!DIAG) {
-        const int64_t gw = select_winner(a.cands_in, a.nranks, D, a.cand_stride, s_row, &s_gidx);
+        const int64_t gw = pick_winner<true, D>(a.recs_in, a.nrecs_in, a.rec_stride, D, s_row,
+                                                s_v, s_i, &s_slot);
         if (blockIdx.x == 0 && threadIdx.x == 0 && a.idx_out) a.idx_out[a.t - 1] = (uint32_t)gw;
 #pragma unroll
         for (int k = 0; k < D; ++k) { xj[k] = s_row[k]; gj[k] = s_row[D + k]; }
         if constexpr (GF) wj = s_row[2 * D];
+    } else {
+#pragma unroll
+        for (int k = 0; k < D; ++k) { xj[k] = 0.0; gj[k] = 0.0; }
     }
 
-    const int64_t n = a.n, ld = a.ld;
     const double l = a.l, l2 = a.l * a.l, tr = a.tr;
     double best_v = INFINITY;
     int64_t best_i = INT64_MAX;
-    const int64_t npairs = (n + 1) >> 1;
-    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < npairs;
-         p += (int64_t)gridDim.x * kBlock) {
-        const int64_t i0 = p * 2;
-        double x0[D], x1[D], g0[D], g1[D];
-#pragma unroll
-        for (int k = 0; k < D; ++k) {
-            const double2 xv = *reinterpret_cast<const double2*>(a.x + k * ld + i0);
-            const double2 gv = *reinterpret_cast<const double2*>(a.g + k * ld + i0);
-            x0[k] = xv.x; x1[k] = xv.y; g0[k] = gv.x; g1[k] = gv.y;
+    if constexpr (PF) {
+        while (u < nunits) {
+            const int64_t un = u + ustride;
+            T nxt;
+            if (un < nunits) load_tile<D, GF, DIAG, CPT>(a, un * CPT, nxt);
+            eval_tile<D, GF, DIAG, CPT>(a, u * CPT, cur, xj, gj, wj, l, l2, tr, best_v, best_i);
+            cur = nxt;
+            u = un;
         }
-        double2 w2 = make_double2(1.0, 1.0);
-        if constexpr (GF) w2 = *reinterpret_cast<const double2*>(a.w + i0);
-        double k0v, k1v;
-        if constexpr (DIAG) {
-            k0v = diag_value_ct<D>(g0, tr);
-            k1v = diag_value_ct<D>(g1, tr);
-            if constexpr (GF) {
-                k0v = (k0v * w2.x) * w2.x;
-                k1v = (k1v * w2.y) * w2.y;
-            }
-        } else {
-            k0v = pair_value_ct<D>(x0, g0, xj, gj, l, l2, tr);
-            k1v = pair_value_ct<D>(x1, g1, xj, gj, l, l2, tr);
-            if constexpr (GF) {
-                k0v = (k0v * w2.x) * wj;
-                k1v = (k1v * w2.y) * wj;
-            }
+    } else {
+        for (; u < nunits; u += ustride) {
+            load_tile<D, GF, DIAG, CPT>(a, u * CPT, cur);
+            eval_tile<D, GF, DIAG, CPT>(a, u * CPT, cur, xj, gj, wj, l, l2, tr, best_v, best_i);
         }
-        double2 av;
-        if constexpr (DIAG) {
-            av = make_double2(k0v, k1v);
-        } else {
-            av = *reinterpret_cast<const double2*>(a.A + i0);
-            av.x = av.x + 2.0 * k0v;
-            av.y = av.y + 2.0 * k1v;
-        }
-        *reinterpret_cast<double2*>(a.A + i0) = av;
-        if (better(av.x, i0, best_v, best_i)) { best_v = av.x; best_i = i0; }
-        if (i0 + 1 < n && better(av.y, i0 + 1, best_v, best_i)) { best_v = av.y; best_i = i0 + 1; }
     }
-    block_minloc(best_v, best_i, s_v, s_i);
-    if (arrive(a, best_v, best_i, &s_flag)) publish_rank_candidate(a, s_v, s_i);
+    write_block_record(a, best_v, best_i, s_v, s_i);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -209,14 +262,14 @@ __global__ __launch_bounds__(kBlock) void greedy_step_ct(GreedyArgs a) {
 template <bool GF, bool DIAG>
 __global__ __launch_bounds__(kBlock) void greedy_step_rt(GreedyArgs a) {
     __shared__ double s_row[2 * kMaxDim + 1];
-    __shared__ int64_t s_gidx;
     __shared__ double s_v[kWaves];
     __shared__ int64_t s_i[kWaves];
-    __shared__ int s_flag;
+    __shared__ int s_slot;
     const int d = a.d;
     double wj = 1.0;
     if constexpr (!DIAG) {
-        const int64_t gw = select_winner(a.cands_in, a.nranks, d, a.cand_stride, s_row, &s_gidx);
+        const int64_t gw = pick_winner<false, 1>(a.recs_in, a.nrecs_in, a.rec_stride, d, s_row,
+                                                 s_v, s_i, &s_slot);
         if (blockIdx.x == 0 && threadIdx.x == 0 && a.idx_out) a.idx_out[a.t - 1] = (uint32_t)gw;
         if constexpr (GF) wj = s_row[2 * d];
     }
@@ -239,58 +292,119 @@ __global__ __launch_bounds__(kBlock) void greedy_step_rt(GreedyArgs a) {
         }
         if (better(kv, i, best_v, best_i)) { best_v = kv; best_i = i; }
     }
-    block_minloc(best_v, best_i, s_v, s_i);
-    if (arrive(a, best_v, best_i, &s_flag)) publish_rank_candidate(a, s_v, s_i);
+    write_block_record(a, best_v, best_i, s_v, s_i);
 }
 
-// K3: after the last step's exchange, write idx[m-1].
-__global__ void greedy_finalize(const double* cands, int nranks, int64_t stride, uint32_t* idx_out,
-                                int64_t t) {
+// R > 1 ranks: reduce this rank's K block records to ONE rank record (the all-gather payload).
+__global__ __launch_bounds__(kBlock) void greedy_publish(const double* __restrict__ recs, int K,
+                                                        int64_t stride, int d,
+                                                        double* __restrict__ out) {
+    __shared__ double s_v[kWaves];
+    __shared__ int64_t s_i[kWaves];
+    __shared__ int s_slot;
     double v = INFINITY;
     int64_t gi = INT64_MAX;
-    if ((int)threadIdx.x < nranks) {
-        v = cands[threadIdx.x * stride];
-        gi = (int64_t)__double_as_longlong(cands[threadIdx.x * stride + 1]);
+    int slot = -1;
+    for (int r = threadIdx.x; r < K; r += kBlock) {
+        const double rv = recs[(int64_t)r * stride];
+        const int64_t ri = rec_gidx(recs + (int64_t)r * stride);
+        if (better(rv, ri, v, gi)) { v = rv; gi = ri; slot = r; }
     }
-    wave_minloc(v, gi);
+    double bv = v;
+    int64_t bi = gi;
+    block_minloc(bv, bi, s_v, s_i);
+    if (slot >= 0 && gi == bi) s_slot = slot;
+    __syncthreads();
+    const double* src = recs + (int64_t)s_slot * stride;
+    for (int k = threadIdx.x; k < 2 * d + 1 + kCandHeader; k += kBlock) out[k] = src[k];
+}
+
+// K3: idx[t] from the K records of the last launch (or the last all-gather).
+__global__ __launch_bounds__(kBlock) void greedy_finalize(const double* __restrict__ recs, int K,
+                                                         int64_t stride, uint32_t* idx_out,
+                                                         int64_t t) {
+    __shared__ double s_v[kWaves];
+    __shared__ int64_t s_i[kWaves];
+    double v = INFINITY;
+    int64_t gi = INT64_MAX;
+    for (int r = threadIdx.x; r < K; r += kBlock) {
+        const double rv = recs[(int64_t)r * stride];
+        const int64_t ri = rec_gidx(recs + (int64_t)r * stride);
+        if (better(rv, ri, v, gi)) { v = rv; gi = ri; }
+    }
+    block_minloc(v, gi, s_v, s_i);
     if (threadIdx.x == 0) idx_out[t] = (uint32_t)gi;
 }
 
 // ------------------------------------------------------------------------------------------
-// host-side launchers
+// host-side launchers; tuning state set by st_tune (defaults: measured best on MI355X)
 // ------------------------------------------------------------------------------------------
+static int g_max_blocks = 256;
+static int g_cpt = 2;
+static int g_pf = 0;
+
+int tune(int key, int value) {
+    switch (key) {
+        case 0: if (value < 1 || value > kMaxBlocks) return -1; g_max_blocks = value; return 0;
+        case 1: if (value != 1 && value != 2 && value != 4) return -1; g_cpt = value; return 0;
+        case 2: g_pf = value ? 1 : 0; return 0;
+        default: return -1;
+    }
+}
+
+// candidates per lane of the kernel variant launched for dimension d
+static int cpt_for(int d) {
+    if (d == 2 || d == 4) return g_cpt;
+    return d <= kMaxCtDim ? 2 : 1;
+}
+
 int greedy_blocks(int64_t n, int d) {
-    const int64_t per_block = (d <= kMaxCtDim ? 2 : 1) * (int64_t)kBlock;
+    const int64_t per_block = (int64_t)cpt_for(d) * kBlock;
     int64_t b = (n + per_block - 1) / per_block;
-    if (b > kMaxBlocks) b = kMaxBlocks;
+    if (b > g_max_blocks) b = g_max_blocks;
     if (b < 1) b = 1;
     return (int)b;
 }
 
-template <int D>
-static hipError_t launch_ct(const GreedyArgs& a, bool diag, int blocks, hipStream_t s) {
+template <int D, int CPT, bool PF>
+static void launch_ct3(const GreedyArgs& a, bool diag, int blocks, hipStream_t s) {
     const bool gf = a.w != nullptr;
     if (diag) {
-        if (gf) greedy_step_ct<D, true, true><<<blocks, kBlock, 0, s>>>(a);
-        else greedy_step_ct<D, false, true><<<blocks, kBlock, 0, s>>>(a);
+        if (gf) greedy_step_ct<D, true, true, CPT, PF><<<blocks, kBlock, 0, s>>>(a);
+        else greedy_step_ct<D, false, true, CPT, PF><<<blocks, kBlock, 0, s>>>(a);
     } else {
-        if (gf) greedy_step_ct<D, true, false><<<blocks, kBlock, 0, s>>>(a);
-        else greedy_step_ct<D, false, false><<<blocks, kBlock, 0, s>>>(a);
+        if (gf) greedy_step_ct<D, true, false, CPT, PF><<<blocks, kBlock, 0, s>>>(a);
+        else greedy_step_ct<D, false, false, CPT, PF><<<blocks, kBlock, 0, s>>>(a);
     }
-    return hipGetLastError();
 }
 
-hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, hipStream_t s) {
-    const int blocks = greedy_blocks(a.n, a.d);
+template <int D>
+static void launch_ct(const GreedyArgs& a, bool diag, int blocks, hipStream_t s) {
+    if constexpr (D == 2 || D == 4) {   // full variant set (tuning sweeps)
+        switch (g_cpt * 2 + g_pf) {
+            case 2: launch_ct3<D, 1, false>(a, diag, blocks, s); break;
+            case 3: launch_ct3<D, 1, true>(a, diag, blocks, s); break;
+            case 4: launch_ct3<D, 2, false>(a, diag, blocks, s); break;
+            case 5: launch_ct3<D, 2, true>(a, diag, blocks, s); break;
+            case 8: launch_ct3<D, 4, false>(a, diag, blocks, s); break;
+            default: launch_ct3<D, 4, true>(a, diag, blocks, s); break;
+        }
+    } else {
+        if (g_pf) launch_ct3<D, 2, true>(a, diag, blocks, s);
+        else launch_ct3<D, 2, false>(a, diag, blocks, s);
+    }
+}
+
+hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStream_t s) {
     switch (a.d) {
-        case 1: return launch_ct<1>(a, diag, blocks, s);
-        case 2: return launch_ct<2>(a, diag, blocks, s);
-        case 3: return launch_ct<3>(a, diag, blocks, s);
-        case 4: return launch_ct<4>(a, diag, blocks, s);
-        case 5: return launch_ct<5>(a, diag, blocks, s);
-        case 6: return launch_ct<6>(a, diag, blocks, s);
-        case 7: return launch_ct<7>(a, diag, blocks, s);
-        case 8: return launch_ct<8>(a, diag, blocks, s);
+        case 1: launch_ct<1>(a, diag, blocks, s); return hipGetLastError();
+        case 2: launch_ct<2>(a, diag, blocks, s); return hipGetLastError();
+        case 3: launch_ct<3>(a, diag, blocks, s); return hipGetLastError();
+        case 4: launch_ct<4>(a, diag, blocks, s); return hipGetLastError();
+        case 5: launch_ct<5>(a, diag, blocks, s); return hipGetLastError();
+        case 6: launch_ct<6>(a, diag, blocks, s); return hipGetLastError();
+        case 7: launch_ct<7>(a, diag, blocks, s); return hipGetLastError();
+        case 8: launch_ct<8>(a, diag, blocks, s); return hipGetLastError();
         default: break;
     }
     const bool gf = a.w != nullptr;
@@ -304,9 +418,15 @@ hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, hipStream_t s) {
     return hipGetLastError();
 }
 
-hipError_t launch_greedy_finalize(const double* cands, int nranks, int64_t stride,
-                                  uint32_t* idx_out, int64_t t, hipStream_t s) {
-    greedy_finalize<<<1, 64, 0, s>>>(cands, nranks, stride, idx_out, t);
+hipError_t launch_greedy_publish(const double* recs, int K, int64_t stride, int d, double* out,
+                                 hipStream_t s) {
+    greedy_publish<<<1, kBlock, 0, s>>>(recs, K, stride, d, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_greedy_finalize(const double* recs, int K, int64_t stride, uint32_t* idx_out,
+                                  int64_t t, hipStream_t s) {
+    greedy_finalize<<<1, kBlock, 0, s>>>(recs, K, stride, idx_out, t);
     return hipGetLastError();
 }
 

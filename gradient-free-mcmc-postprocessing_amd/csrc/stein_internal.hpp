@@ -18,26 +18,26 @@ struct GreedyArgs {
     const double* w;      // (ld) gradient-free weights, or nullptr for the Langevin kernel
     double* A;            // (ld) running sums, in place
     int64_t n;            // rows in this shard
-    int64_t ld;           // leading dimension (even, >= n + (n & 1))
+    int64_t ld;           // leading dimension (multiple of 8, >= n)
     int d;
     double l;             // isotropic preconditioner Gamma^-1 = l * I
     double tr;            // np.trace(Gamma^-1), computed on the host exactly as the reference
     int64_t row_offset;   // global index of shard row 0
-    const double* cands_in;  // R candidate records of the previous step (unused for the diagonal)
-    int nranks;
-    int64_t cand_stride;
-    double* cand_out;     // this rank's candidate record for this step
+    const double* recs_in;  // K candidate records of the previous step (unused for the diagonal)
+    int nrecs_in;
+    int64_t rec_stride;   // doubles per record
+    double* recs_out;     // one record per block of this launch
     uint32_t* idx_out;    // device index array; launch t writes idx[t-1]
     int64_t t;            // step being computed (0 = diagonal)
-    double* part_val;     // per-block partial MINLOC
-    int64_t* part_idx;
-    unsigned* ticket;     // monotone arrival counter, zeroed once per greedy run
 };
 
 int greedy_blocks(int64_t n, int d);
-hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, hipStream_t s);
-hipError_t launch_greedy_finalize(const double* cands, int nranks, int64_t stride,
-                                  uint32_t* idx_out, int64_t t, hipStream_t s);
+int tune(int key, int value);
+hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStream_t s);
+hipError_t launch_greedy_publish(const double* recs, int K, int64_t stride, int d, double* out,
+                                 hipStream_t s);
+hipError_t launch_greedy_finalize(const double* recs, int K, int64_t stride, uint32_t* idx_out,
+                                  int64_t t, hipStream_t s);
 
 struct PairArgs {
     const double* x;

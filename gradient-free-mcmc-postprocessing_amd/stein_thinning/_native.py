@@ -34,8 +34,11 @@ SIGNATURES = {
     'st_last_error': (ctypes.c_char_p, []),
     'st_greedy_workspace_bytes': (_i64, [_i64, _i32, _i32]),
     'st_candidate_stride': (_i64, [_i32]),
+    'st_tune': (ctypes.c_int, [_i32, _i32]),
     'st_greedy': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64, _i64,
                                  _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
+    'st_greedy_steps': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64, _i64,
+                                       _i64, _i64, _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
     'st_greedy_step': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
                                       _i64, _i64, _i32, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp,
                                       _i64, _c_dp]),

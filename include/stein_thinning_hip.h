@@ -12,7 +12,8 @@
  *   - `stream` is a hipStream_t (NULL = default stream); every function is asynchronous on it,
  *     allocates nothing and never synchronises (graph-capturable);
  *   - sample / gradient arrays are SoA: element (i, k) of the (n, d) array lives at p[k * ld + i],
- *     ld even and >= n + (n & 1); per-row arrays (weights, running sums) have ld entries;
+ *     ld a multiple of 8 and >= n; per-row arrays (weights, running sums) have ld entries (rows
+ *     n..ld-1 are padding: read, and in the running sums overwritten, never selected);
  *     all device pointers 16-byte aligned;
  *   - the preconditioner is isotropic Gamma^-1 = linv_scale * I ('id', 'med', 'sclmed', float
  *     options of the reference); linv_trace = np.trace(Gamma^-1) computed on the host;
@@ -47,8 +48,15 @@ const char *st_last_error(void);
  * _make_stein_gf_integrand (called at code/src/utils/ksd.py:25, Gaussian_mixture.ipynb cell 93).
  * ---------------------------------------------------------------------------------------- */
 
-/* bytes of device workspace st_greedy / st_greedy_step need (zeroing is done internally) */
+/* bytes of device workspace st_greedy / st_greedy_steps / st_greedy_step need (no zeroing needed) */
 int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
+
+/*
+ * Kernel-variant tuning (process-wide, host side; for measurement sweeps -- defaults are the
+ * measured best on MI355X): key 0 = grid cap (blocks, 1..1024), key 1 = candidates per lane
+ * (1, 2, 4; d = 2 and 4 kernels), key 2 = register prefetch of the next tile (0/1).
+ */
+int st_tune(int32_t key, int32_t value);
 
 /* doubles per rank-candidate record {value, global index bits, x[d], g[d], w} (even) */
 int64_t st_candidate_stride(int32_t d);
@@ -64,11 +72,23 @@ int st_greedy(const double *x_soa, const double *g_soa, const double *weights, i
               void *stream);
 
 /*
+ * Steps [t_begin, t_end) of the same single-device run (t = 0 is the diagonal); when t_end ==
+ * n_points the finalize kernel writing idx_out[n_points-1] follows.  The workspace carries the
+ * per-block candidate records between calls, so consecutive ranges on one stream compose into
+ * st_greedy.  Used to time single step launches.
+ */
+int st_greedy_steps(const double *x_soa, const double *g_soa, const double *weights, int64_t n,
+                    int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t t_begin,
+                    int64_t t_end, int64_t n_points, uint32_t *idx_out, double *a_work,
+                    void *workspace, int64_t workspace_bytes, void *stream);
+
+/*
  * One greedy step of a row-sharded run (multi-GPU; one process per GPU).  This rank holds rows
  * [row_offset, row_offset + n) of the global sample.  Step t = 0 evaluates the diagonal; step
  * t >= 1 reads the R = nranks candidate records of step t-1 (cands_in, R * stride doubles),
  * writes idx_out[t-1] and updates the running sums.  Every step writes this rank's candidate
- * record to cand_out; the caller all-gathers the records (RCCL) into the next step's cands_in.
+ * record (stride doubles) to cand_out; the caller all-gathers the records (RCCL) into the next
+ * step's cands_in.
  * After the last step, st_greedy_finalize writes idx_out[n_points-1].
  */
 int st_greedy_step(const double *x_soa, const double *g_soa, const double *weights, int64_t n,

@@ -26,6 +26,6 @@ if [[ $MODE == all || $MODE == bench ]]; then
   step bench 900 python bench.py --steps 3 --warmup 1
 fi
 if [[ $MODE == all || $MODE == prof ]]; then
-  step rocprof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
+  step rocprof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline
 fi
 echo "=== done"

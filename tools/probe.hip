@@ -1,0 +1,163 @@
+// Measurement probe (not product code): achievable bandwidth for the greedy step's exact access
+// pattern on this MI355X, and a sweep of the step-kernel variants exposed by st_tune().
+// Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -o tools/probe tools/probe.hip \
+//        -Lgradient-free-mcmc-postprocessing_amd/stein_thinning/_lib -lstein_hip -Wl,-rpath,<that dir>
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+
+#include <algorithm>
+#include <vector>
+
+#include "../include/stein_thinning_hip.h"
+
+#define CK(x)                                                                   \
+    do {                                                                        \
+        hipError_t e_ = (x);                                                    \
+        if (e_ != hipSuccess) {                                                 \
+            fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+            exit(1);                                                            \
+        }                                                                       \
+    } while (0)
+
+__global__ void fill(double* p, int64_t n, uint64_t seed, double scale) {
+    for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        uint64_t z = (uint64_t)i * 0x9E3779B97F4A7C15ull + seed;
+        z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+        z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+        z ^= z >> 31;
+        p[i] = ((double)(z >> 11) * 0x1.0p-53 - 0.5) * scale;
+    }
+}
+
+// pure streaming of the step's traffic: 2*D column reads (+A read, +A write), double2 per lane
+template <int D, bool WRITE_A, int CPT>
+__global__ __launch_bounds__(256) void stream_kernel(const double* x, const double* g, double* A,
+                                                     int64_t n, int64_t ld, double* out) {
+    double acc = 0.0;
+    const int64_t nunits = n / CPT;
+    for (int64_t u = blockIdx.x * 256ll + threadIdx.x; u < nunits; u += (int64_t)gridDim.x * 256) {
+        const int64_t i0 = u * CPT;
+        double s[CPT];
+#pragma unroll
+        for (int c = 0; c < CPT; ++c) s[c] = 0.0;
+#pragma unroll
+        for (int k = 0; k < D; ++k)
+#pragma unroll
+            for (int c = 0; c < CPT; c += 2) {
+                const double2 xv = *reinterpret_cast<const double2*>(x + k * ld + i0 + c);
+                const double2 gv = *reinterpret_cast<const double2*>(g + k * ld + i0 + c);
+                s[c] += xv.x * gv.x;
+                s[c + 1] += xv.y * gv.y;
+            }
+#pragma unroll
+        for (int c = 0; c < CPT; c += 2) {
+            double2 av = *reinterpret_cast<const double2*>(A + i0 + c);
+            if (WRITE_A) {
+                av.x += s[c];
+                av.y += s[c + 1];
+                *reinterpret_cast<double2*>(A + i0 + c) = av;
+            } else {
+                acc += av.x + av.y + s[c] + s[c + 1];
+            }
+        }
+    }
+    if (!WRITE_A && acc == 12345.678) out[0] = acc;
+}
+
+struct Timer {
+    hipEvent_t a, b;
+    Timer() { CK(hipEventCreate(&a)); CK(hipEventCreate(&b)); }
+    void start(hipStream_t s) { CK(hipEventRecord(a, s)); }
+    float stop(hipStream_t s) {
+        CK(hipEventRecord(b, s));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms;
+    }
+};
+
+int main(int argc, char** argv) {
+    const int64_t n = argc > 1 ? atoll(argv[1]) : 2000000;
+    const int d = 4;
+    const int64_t ld = (n + 63) / 64 * 64;
+    hipStream_t s;
+    CK(hipStreamCreate(&s));
+    double *x, *g, *A, *out;
+    CK(hipMalloc(&x, sizeof(double) * d * ld));
+    CK(hipMalloc(&g, sizeof(double) * d * ld));
+    CK(hipMalloc(&A, sizeof(double) * ld));
+    CK(hipMalloc(&out, 64));
+    fill<<<1024, 256, 0, s>>>(x, d * ld, 1, 4.0);
+    fill<<<1024, 256, 0, s>>>(g, d * ld, 2, 6.0);
+    fill<<<1024, 256, 0, s>>>(A, ld, 3, 1.0);
+    CK(hipStreamSynchronize(s));
+    Timer T;
+    const double bytes_rw = (double)n * (16 * d + 16), bytes_r = (double)n * (16 * d + 8);
+    printf("# n=%lld d=%d  step traffic %.1f MB (read %.1f MB)\n", (long long)n, d, bytes_rw / 1e6, bytes_r / 1e6);
+    const int reps = 200;
+    for (int blocks : {256, 512, 1024, 2048, 4096}) {
+        for (int wr = 0; wr < 2; ++wr) {
+            for (int cpt : {2, 4}) {
+                auto launch = [&]() {
+                    if (wr) {
+                        if (cpt == 2) stream_kernel<4, true, 2><<<blocks, 256, 0, s>>>(x, g, A, n, ld, out);
+                        else stream_kernel<4, true, 4><<<blocks, 256, 0, s>>>(x, g, A, n, ld, out);
+                    } else {
+                        if (cpt == 2) stream_kernel<4, false, 2><<<blocks, 256, 0, s>>>(x, g, A, n, ld, out);
+                        else stream_kernel<4, false, 4><<<blocks, 256, 0, s>>>(x, g, A, n, ld, out);
+                    }
+                };
+                for (int i = 0; i < 20; ++i) launch();
+                T.start(s);
+                for (int i = 0; i < reps; ++i) launch();
+                const float ms = T.stop(s);
+                const double us = ms * 1e3 / reps;
+                printf("stream blocks=%5d write_A=%d cpt=%d  %8.2f us/launch  %7.1f GB/s\n", blocks, wr, cpt, us,
+                       (wr ? bytes_rw : bytes_r) / (us * 1e-6) / 1e9);
+            }
+        }
+    }
+    // greedy step variants through the C ABI (single-device run of `reps` steps)
+    const int64_t ws_bytes = st_greedy_workspace_bytes(n, d, 1);
+    void* ws;
+    uint32_t* idx;
+    CK(hipMalloc(&ws, ws_bytes));
+    CK(hipMalloc(&idx, 4 * 4096));
+    const double l = 0.37, tr = 4 * 0.37;
+    const int M = reps + 1;
+    for (int blocks : {128, 256, 512, 1024}) {
+        for (int cpt : {1, 2, 4}) {
+            for (int pf = 0; pf < 2; ++pf) {
+                st_tune(0, blocks);
+                st_tune(1, cpt);
+                st_tune(2, pf);
+                auto run = [&](int64_t t0, int64_t t1) {
+                    int rc = st_greedy_steps(x, g, nullptr, n, d, ld, l, tr, t0, t1, M, idx, A, ws, ws_bytes, s);
+                    if (rc) { fprintf(stderr, "rc=%d %s\n", rc, st_last_error()); exit(1); }
+                };
+                run(0, 1);
+                for (int t = 1; t < 11; ++t) run(t, t + 1);
+                T.start(s);
+                run(11, 11 + 150);
+                const double us = T.stop(s) * 1e3 / 150;
+                std::vector<float> v;
+                for (int t = 161; t < 191; ++t) {
+                    T.start(s);
+                    run(t, t + 1);
+                    v.push_back(T.stop(s) * 1e3f);
+                }
+                std::sort(v.begin(), v.end());
+                printf("greedy blocks=%4d cpt=%d pf=%d  %8.2f us/step back-to-back (%7.1f GB/s)  isolated median %8.2f us\n",
+                       blocks, cpt, pf, us, bytes_rw / (us * 1e-6) / 1e9, v[v.size() / 2]);
+            }
+        }
+    }
+    st_tune(0, 256); st_tune(1, 2); st_tune(2, 0);
+    T.start(s);
+    for (int r = 0; r < 50; ++r) st_greedy_steps(x, g, nullptr, n, d, ld, l, tr, 0, 1, M, idx, A, ws, ws_bytes, s);
+    printf("diag  %8.2f us/launch\n", T.stop(s) * 1e3 / 50);
+    return 0;
+}
