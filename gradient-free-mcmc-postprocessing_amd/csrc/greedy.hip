@@ -339,27 +339,39 @@ __global__ __launch_bounds__(kBlock) void greedy_finalize(const double* __restri
 // ------------------------------------------------------------------------------------------
 // host-side launchers; tuning state set by st_tune (defaults: measured best on MI355X)
 // ------------------------------------------------------------------------------------------
+// Defaults measured on MI355X (tools/probe.hip sweeps, DESIGN.md "Tuning"): 256 blocks (one per
+// CU); d = 2/4 shards of >= 1e6 rows: one candidate per lane with register prefetch, smaller
+// shards: two candidates per lane without prefetch.  st_tune overrides (-1 = automatic).
 static int g_max_blocks = 256;
-static int g_cpt = 2;
-static int g_pf = 0;
+static int g_cpt = -1;
+static int g_pf = -1;
+constexpr int64_t kLargeShard = 1000000;
 
 int tune(int key, int value) {
     switch (key) {
         case 0: if (value < 1 || value > kMaxBlocks) return -1; g_max_blocks = value; return 0;
-        case 1: if (value != 1 && value != 2 && value != 4) return -1; g_cpt = value; return 0;
-        case 2: g_pf = value ? 1 : 0; return 0;
+        case 1: if (value != -1 && value != 1 && value != 2 && value != 4) return -1; g_cpt = value; return 0;
+        case 2: if (value < -1 || value > 1) return -1; g_pf = value; return 0;
         default: return -1;
     }
 }
 
-// candidates per lane of the kernel variant launched for dimension d
-static int cpt_for(int d) {
-    if (d == 2 || d == 4) return g_cpt;
-    return d <= kMaxCtDim ? 2 : 1;
+// kernel variant (candidates per lane, prefetch) launched for an (n, d) shard
+static void variant_for(int64_t n, int d, int& cpt, int& pf) {
+    if (d == 2 || d == 4) {
+        const bool large = n >= kLargeShard;
+        cpt = g_cpt > 0 ? g_cpt : (large ? 1 : 2);
+        pf = g_pf >= 0 ? g_pf : (large ? 1 : 0);
+    } else {
+        cpt = d <= kMaxCtDim ? 2 : 1;
+        pf = g_pf > 0 ? 1 : 0;
+    }
 }
 
 int greedy_blocks(int64_t n, int d) {
-    const int64_t per_block = (int64_t)cpt_for(d) * kBlock;
+    int cpt, pf;
+    variant_for(n, d, cpt, pf);
+    const int64_t per_block = (int64_t)cpt * kBlock;
     int64_t b = (n + per_block - 1) / per_block;
     if (b > g_max_blocks) b = g_max_blocks;
     if (b < 1) b = 1;
@@ -380,8 +392,10 @@ static void launch_ct3(const GreedyArgs& a, bool diag, int blocks, hipStream_t s
 
 template <int D>
 static void launch_ct(const GreedyArgs& a, bool diag, int blocks, hipStream_t s) {
-    if constexpr (D == 2 || D == 4) {   // full variant set (tuning sweeps)
-        switch (g_cpt * 2 + g_pf) {
+    int cpt, pf;
+    variant_for(a.n, D, cpt, pf);
+    if constexpr (D == 2 || D == 4) {   // full variant set
+        switch (cpt * 2 + pf) {
             case 2: launch_ct3<D, 1, false>(a, diag, blocks, s); break;
             case 3: launch_ct3<D, 1, true>(a, diag, blocks, s); break;
             case 4: launch_ct3<D, 2, false>(a, diag, blocks, s); break;
@@ -390,7 +404,7 @@ static void launch_ct(const GreedyArgs& a, bool diag, int blocks, hipStream_t s)
             default: launch_ct3<D, 4, true>(a, diag, blocks, s); break;
         }
     } else {
-        if (g_pf) launch_ct3<D, 2, true>(a, diag, blocks, s);
+        if (pf) launch_ct3<D, 2, true>(a, diag, blocks, s);
         else launch_ct3<D, 2, false>(a, diag, blocks, s);
     }
 }

@@ -1,0 +1,13 @@
+#!/usr/bin/env bash
+# Profiling session: bench (full, with CPU baseline) -> kernel trace/stats -> PMC passes (one counter group each).
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+CFG=${1:-c4}
+run() { local name=$1 tmo=$2; shift 2; echo "=== $name ($(date +%T))"; timeout -k 10 "$tmo" "$@" > "gpurun_out/$name.log" 2>&1; local rc=$?; echo "=== $name rc=$rc"; tail -n 5 "gpurun_out/$name.log"; [[ $rc == 0 ]] || exit $rc; }
+run bench_$CFG 900 python bench.py --config $CFG --steps 5 --warmup 2
+run trace_$CFG 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$CFG -o trace -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline
+run pmc_fetch_$CFG 900 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$CFG -o pmc -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-timing
+run pmc_write_$CFG 900 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$CFG -o pmc -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-timing
+echo "=== done"

@@ -155,7 +155,7 @@ int main(int argc, char** argv) {
             }
         }
     }
-    st_tune(0, 256); st_tune(1, 2); st_tune(2, 0);
+    st_tune(0, 256); st_tune(1, -1); st_tune(2, -1);
     T.start(s);
     for (int r = 0; r < 50; ++r) st_greedy_steps(x, g, nullptr, n, d, ld, l, tr, 0, 1, M, idx, A, ws, ws_bytes, s);
     printf("diag  %8.2f us/launch\n", T.stop(s) * 1e3 / 50);
