@@ -141,26 +141,30 @@ def cpu_baseline(cfg, integrand, steps: int):
                        f"({os.cpu_count()} logical CPUs)")}
 
 
-def kernel_timing(prob, n_points: int, repeats: int = 3):
-    """Average duration of the fused step kernel, measured with HIP events around single step
-    launches (st_greedy_steps) on the stream they are launched on."""
+def kernel_timing(prob, n_points: int, repeats: int = 5):
+    """Average duration of the fused step kernel: HIP events on the launch stream bracket a run of
+    back-to-back single-step launches (st_greedy_steps t = 1 .. n_points-1, no other work in
+    between), averaged per launch -- the quantity rocprofv3's kernel-trace average reports."""
     import torch
     from stein_thinning import _native as nat
     L = nat.lib()
     idx, a, ws = prob.greedy_buffers(n_points)
     stream = torch.cuda.current_stream()
-    durs = []
+
+    def steps(t0, t1):
+        nat.check(L.st_greedy_steps(nat.ptr(prob.x), nat.ptr(prob.g), nat.ptr(prob.w), prob.n, prob.d, prob.ld,
+                                    prob.l, prob.tr, t0, t1, n_points, nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
+                                    ws.numel() * 8, nat.stream_handle()), 'st_greedy_steps')
+    per = []
     for _ in range(repeats):
-        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(n_points)]
-        for t in range(n_points):
-            evs[t][0].record(stream)
-            nat.check(L.st_greedy_steps(nat.ptr(prob.x), nat.ptr(prob.g), nat.ptr(prob.w), prob.n, prob.d, prob.ld,
-                                        prob.l, prob.tr, t, t + 1, n_points, nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
-                                        ws.numel() * 8, nat.stream_handle()), 'st_greedy_steps')
-            evs[t][1].record(stream)
+        steps(0, 1)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        steps(1, n_points - 1)
+        e1.record(stream)
         torch.cuda.synchronize()
-        durs.extend(e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs[1:-1])   # streaming steps only
-    return float(np.mean(durs)), float(np.median(durs))
+        per.append(e0.elapsed_time(e1) * 1e-3 / (n_points - 2))
+    return float(np.mean(per)), float(np.median(per))
 
 
 def main():
@@ -172,6 +176,8 @@ def main():
     ap.add_argument('--cpu-steps', type=int, default=60, help='greedy steps of the CPU baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--no-graph', action='store_true', help='N > 1: eager per-step launches instead of a HIP graph')
+    ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     args = ap.parse_args()
 
     import torch
@@ -181,7 +187,12 @@ def main():
     local = int(os.environ.get('LOCAL_RANK', 0))
     torch.cuda.set_device(local)
     dev = torch.device('cuda', local)
-    if world > 1:
+    sharded = world > 1 or args.sharded
+    if sharded:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29531')
+        os.environ.setdefault('RANK', str(rank))
+        os.environ.setdefault('WORLD_SIZE', str(world))
         dist.init_process_group('nccl', device_id=dev)
 
     cfg = CONFIGS[args.config]
@@ -189,28 +200,25 @@ def main():
     integrand, _, _ = make_integrand(cfg)
     d = integrand.sample.shape[1]
 
-    if world == 1:
+    if not sharded:
         prob = integrand.device_problem()
         idx, a, ws = prob.greedy_buffers(m)
 
         def run_once():
             prob.greedy_launch(m, idx, a, ws)
     else:
-        from stein_thinning.distributed import HipShardBackend, run_sharded, shard_bounds
+        from stein_thinning.distributed import GraphedShardedGreedy, HipShardBackend, shard_bounds
         r0, r1 = shard_bounds(n, rank, world)
         backend = HipShardBackend(integrand, r0, r1, world, m)
+        runner = GraphedShardedGreedy(backend, m, use_graph=not args.no_graph)
 
         def run_once():
-            for t in range(m):
-                backend.step(t)
-                dist.all_gather_into_tensor(backend.recv, backend.send)
-            backend.finalize(m - 1)
-        _ = run_sharded
+            runner.launch()
 
     for _ in range(args.warmup):
         run_once()
     torch.cuda.synchronize()
-    if world > 1:
+    if sharded:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -218,13 +226,13 @@ def main():
         run_once()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    if world > 1:
+    if sharded:
         dist.barrier()
         tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         dist.all_reduce(tt, op=dist.ReduceOp.MAX)
         elapsed = float(tt.item())
 
-    if world == 1:
+    if not sharded:
         result_idx = idx.cpu().numpy().view(np.uint32)
     else:
         result_idx = backend.indices()
@@ -233,7 +241,7 @@ def main():
     cpu = None
     if rank == 0:
         bytes_per_pair = 16 * d + (24 if integrand.weights is not None else 16)
-        if world == 1 and not args.no_kernel_timing:
+        if not sharded and not args.no_kernel_timing:
             avg, med = kernel_timing(prob, min(m, 200))
             alg_bytes = n * bytes_per_pair
             achieved = alg_bytes / avg / 1e9
@@ -242,11 +250,12 @@ def main():
             if os.path.exists(pmc):
                 rec = json.load(open(pmc)).get(args.config)
                 if rec:
-                    traffic = rec.get('hbm_bytes_per_launch')
+                    traffic = round(rec.get('hbm_bytes_per_launch'))
             roofline = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                         'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
                         'kernel': f'greedy_step_ct<{d}>' if d <= 8 else 'greedy_step_rt',
                         'kernel_avg_us': round(avg * 1e6, 2), 'kernel_median_us': round(med * 1e6, 2),
+                        'timing': 'HIP events around 198 back-to-back step launches, per-launch mean',
                         'algorithmic_bytes_per_launch': alg_bytes,
                         'bytes_per_pair': bytes_per_pair}
         if world == 1 and not args.no_cpu_baseline:
@@ -269,14 +278,15 @@ def main():
             'data': 'synthetic (seeded RW-MH LV-surrogate chains; see bench.py docstring)',
             'config': {'workload': f"config {args.config[1]}: {cfg['desc']}", 'n': n, 'd': d, 'm': m,
                        'preconditioner': 'med', 'kernel': 'gradient-free' if integrand.weights is not None else 'langevin',
-                       'parallelism': f'rows-sharded x{world}' if world > 1 else 'single-gpu',
+                       'parallelism': (f'rows-sharded x{world}, RCCL record all-gather per step, {runner.mode}'
+                                       if sharded else 'single-gpu'),
                        'wallclock_thin_s': elapsed / args.steps,
                        'first_indices': result_idx[:8].tolist()},
             'roofline': roofline,
             'cpu_baseline': cpu,
         }
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if sharded:
         dist.destroy_process_group()
 
 

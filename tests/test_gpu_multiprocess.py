@@ -1,0 +1,69 @@
+"""Multi-process sharded thinning on the GPU box: 2 ranks (processes) on the one visible GPU,
+exchanging candidate records through gloo (RCCL cannot place two ranks on one device), and a
+1-rank RCCL run of the HIP-graph-captured loop (step + publish + all-gather per step)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+if not torch.cuda.is_available():
+    pytest.skip('no HIP device', allow_module_level=True)
+
+import torch.distributed as dist  # noqa: E402
+import torch.multiprocessing as mp  # noqa: E402
+
+from oracle import stein_numpy as o  # noqa: E402
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _data():
+    rng = np.random.default_rng(5)
+    n, d = 40_003, 4
+    x = rng.normal(size=(n, d))
+    x[30_000:30_400] = x[2_000:2_400]      # exact ties across the shard boundary
+    g = -x + 0.1 * rng.normal(size=(n, d))
+    g[30_000:30_400] = g[2_000:2_400]
+    log_p = -0.5 * np.sum(x * x, axis=1)
+    log_q = -0.45 * np.sum(x * x, axis=1)
+    return x, g, log_p, log_q
+
+
+def _worker(rank, world, port, backend, gf, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    kw = dict(device_id=torch.device('cuda', 0)) if backend == 'nccl' else {}
+    dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    try:
+        from stein_thinning.distributed import thin_gf_sharded, thin_sharded
+        x, g, log_p, log_q = _data()
+        if gf:
+            idx = thin_gf_sharded(x, log_p, log_q, g, 80, preconditioner='med')
+        else:
+            idx = thin_sharded(x, g, 80, preconditioner='med')
+        np.save(os.path.join(out_dir, f'idx{rank}.npy'), idx)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('gf', [False, True])
+def test_two_processes_one_gpu_gloo(tmp_path, gf):
+    mp.spawn(_worker, args=(2, _free_port(), 'gloo', gf, str(tmp_path)), nprocs=2, join=True)
+    x, g, log_p, log_q = _data()
+    want = o.thin_gf(x, log_p, log_q, g, 80, preconditioner='med') if gf else o.thin(x, g, 80, preconditioner='med')
+    for r in range(2):
+        np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}.npy'), want)
+
+
+def test_single_rank_rccl_graph_capture(tmp_path):
+    mp.spawn(_worker, args=(1, _free_port(), 'nccl', False, str(tmp_path)), nprocs=1, join=True)
+    x, g, _, _ = _data()
+    np.testing.assert_array_equal(np.load(tmp_path / 'idx0.npy'), o.thin(x, g, 80, preconditioner='med'))
