@@ -41,11 +41,15 @@ int check_problem(const double* x, const double* g, const double* w, int64_t n, 
     return ST_OK;
 }
 
-// workspace layout: two ping-pong banks of per-block candidate records, kMaxBlocks x stride each
-int64_t greedy_ws_bytes(int32_t d) { return 2 * (int64_t)st::kMaxBlocks * st::cand_stride(d) * 8; }
+// workspace layout: [control block (persistent kernel counters/status)][two ping-pong banks of
+// per-block candidate records, kMaxBlocks x stride doubles each]
+int64_t greedy_ws_bytes(int32_t d) {
+    return st::kWsControlBytes + 2 * (int64_t)st::kMaxBlocks * st::cand_stride(d) * 8;
+}
 
 double* bank(void* ws, int32_t d, int b) {
-    return static_cast<double*>(ws) + (int64_t)b * st::kMaxBlocks * st::cand_stride(d);
+    return reinterpret_cast<double*>(static_cast<char*>(ws) + st::kWsControlBytes) +
+           (int64_t)b * st::kMaxBlocks * st::cand_stride(d);
 }
 
 st::GreedyArgs make_args(const double* x, const double* g, const double* w, int64_t n, int32_t d,
@@ -73,7 +77,8 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks) {
 }
 
 int st_tune(int32_t key, int32_t value) {
-    if (st::tune(key, value) != 0) return fail(ST_ERR_INVALID, "bad tuning key/value %d=%d", key, value);
+    const int rc = key == 3 ? st::persistent_tune(value) : st::tune(key, value);
+    if (rc != 0) return fail(ST_ERR_INVALID, "bad tuning key/value %d=%d", key, value);
     return ST_OK;
 }
 
@@ -120,6 +125,20 @@ int st_greedy(const double* x_soa, const double* g_soa, const double* weights, i
               uint32_t* idx_out, double* a_work, void* workspace, int64_t workspace_bytes,
               void* stream) {
     if (n_points < 1) return fail(ST_ERR_INVALID, "n_points must be >= 1");
+    int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
+    if (rc) return rc;
+    if (!idx_out || !a_work || !workspace) return fail(ST_ERR_INVALID, "NULL output/workspace");
+    if (!aligned16(a_work) || !aligned16(workspace))
+        return fail(ST_ERR_INVALID, "a_work/workspace must be 16-byte aligned");
+    if (workspace_bytes < greedy_ws_bytes(d))
+        return fail(ST_ERR_INVALID, "workspace too small (%lld < %lld)", (long long)workspace_bytes,
+                    (long long)greedy_ws_bytes(d));
+    int used = 0;
+    const hipError_t pe = st::launch_greedy_persistent(
+        x_soa, g_soa, weights, a_work, n, d, ld, linv_scale, linv_trace, n_points, idx_out, workspace,
+        workspace_bytes, static_cast<hipStream_t>(stream), &used);
+    if (used) return ST_OK;
+    if (pe != hipErrorNotSupported) (void)hipGetLastError();   // clear a failed cooperative launch
     return st_greedy_steps(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, 0, n_points,
                            n_points, idx_out, a_work, workspace, workspace_bytes, stream);
 }

@@ -9,6 +9,7 @@ constexpr int kMaxDim = 128;     // NumPy pairwise_sum modelled without recursio
 constexpr int kMaxCtDim = 8;     // compile-time-d kernels for d <= 8
 constexpr int kMaxBlocks = 1024; // greedy step grid cap (4 x 256-thread blocks per CU)
 constexpr int kCandHeader = 2;   // candidate record: {val, gidx(bits)} then x[d], g[d], w
+constexpr int64_t kWsControlBytes = 8 * 128 + 128;   // persistent kernel: arrival counters + status
 
 inline int64_t cand_stride(int d) { return ((kCandHeader + 2 * d + 1) + 1) & ~int64_t(1); }
 
@@ -33,6 +34,12 @@ struct GreedyArgs {
 
 int greedy_blocks(int64_t n, int d);
 int tune(int key, int value);
+int persistent_tune(int value);
+int64_t persistent_ws_bytes(int d, int G);
+hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
+                                    int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
+                                    uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
+                                    int* used);
 hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStream_t s);
 hipError_t launch_greedy_publish(const double* recs, int K, int64_t stride, int d, double* out,
                                  hipStream_t s);

@@ -94,6 +94,9 @@ class DeviceProblem:
         idx, a, ws = self.greedy_buffers(n_points)
         self.greedy_launch(n_points, idx, a, ws)
         out = idx.cpu().numpy().view(np.uint32).copy()
+        if out.size and int(out.max()) >= self.n:
+            raise nat.HipExtensionError('greedy kernel did not complete (persistent-kernel wait timed '
+                                        'out); indices poisoned')
         if return_sums:
             return out, a[:self.n].cpu().numpy()
         return out

@@ -55,7 +55,8 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * Kernel-variant tuning (process-wide, host side; for measurement sweeps -- defaults are the
  * measured best on MI355X): key 0 = grid cap (blocks, 1..1024), key 1 = candidates per lane
  * (1, 2, 4; d = 2 and 4 kernels; -1 = automatic), key 2 = register prefetch of the next tile
- * (0/1; -1 = automatic).
+ * (0/1; -1 = automatic), key 3 = persistent kernel register rows per thread (4, 8, 16;
+ * -1 = automatic, 0 = disable the persistent kernel).
  */
 int st_tune(int32_t key, int32_t value);
 
@@ -66,6 +67,10 @@ int64_t st_candidate_stride(int32_t d);
  * Whole greedy run on one device: idx_out[0..n_points) (device, uint32) receives the selected
  * row indices exactly as the reference's `thin` / `thin_gf` / `_greedy_search` return them;
  * a_work (ld doubles, device) ends holding the running sums A after the last step.
+ * For d = 2 and 4 the run is ONE cooperative launch of the persistent on-chip-resident kernel
+ * (one block per CU; rows held in VGPRs/LDS across steps); if its internal bounded wait times
+ * out, the unwritten entries of idx_out are set to UINT32_MAX (callers check idx < n).
+ * Other d: one fused launch per step.
  */
 int st_greedy(const double *x_soa, const double *g_soa, const double *weights, int64_t n,
               int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t n_points,

@@ -144,6 +144,36 @@ def test_running_sums_bit_exact_vs_c_model(d, gf):
     assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
 
 
+@pytest.mark.parametrize('tune', [
+    ('persistent: registers + LDS + streamed rows', 4, 1_000_003, 4),
+    ('persistent: registers only', 16, 30_011, 4),
+    ('persistent: d=2 gradient-free', -1, 200_003, 2),
+    ('launch-per-step path', 0, 300_007, 4),
+])
+def test_persistent_and_fallback_bit_exact(tune):
+    """st_greedy's two implementations (persistent on-chip kernel / one launch per step) against
+    the C model: identical indices and bit-identical running sums."""
+    from stein_thinning import _native
+    _, rt, n, d = tune
+    m = 30
+    x, g = _rw_chain(n, d, seed=n % 97)
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    w = None
+    if d == 2:
+        lw = -0.2 * np.sum(x * x, axis=1)
+        w = np.exp(lw - lw.min())
+    _native.lib().st_tune(3, rt)
+    try:
+        idx, A = DeviceProblem(s, gs, w, l, tr).greedy(m, return_sums=True)
+    finally:
+        _native.lib().st_tune(3, -1)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    np.testing.assert_array_equal(idx, cidx)
+    assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
+
+
 @pytest.mark.parametrize('d', [2, 4, 9, 50])
 def test_pair_values_bit_exact_vs_c_model(d):
     x, g = _rw_chain(700, d, seed=100 + d)

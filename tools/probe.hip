@@ -156,6 +156,22 @@ int main(int argc, char** argv) {
         }
     }
     st_tune(0, 256); st_tune(1, -1); st_tune(2, -1);
+    // whole-run st_greedy: persistent kernel (register rows per thread rt; 0 = launch per step)
+    for (int rt : {16, 8, 4, 0}) {
+        st_tune(3, rt);
+        for (int rep = 0; rep < 3; ++rep) {
+            T.start(s);
+            int rc = st_greedy(x, g, nullptr, n, d, ld, l, tr, M, idx, A, ws, ws_bytes, s);
+            if (rc) { fprintf(stderr, "rc=%d %s\n", rc, st_last_error()); exit(1); }
+            const float ms = T.stop(s);
+            std::vector<uint32_t> h(M);
+            CK(hipMemcpy(h.data(), idx, 4 * M, hipMemcpyDeviceToHost));
+            const uint32_t mx = *std::max_element(h.begin(), h.end());
+            printf("st_greedy rt=%2d m=%d  %8.3f ms  %8.2f us/step  idx[0..2]=%u %u %u  max=%u%s\n", rt, M, ms,
+                   ms * 1e3 / M, h[0], h[1], h[2], mx, mx >= n ? "  POISONED" : "");
+        }
+    }
+    st_tune(3, -1);
     T.start(s);
     for (int r = 0; r < 50; ++r) st_greedy_steps(x, g, nullptr, n, d, ld, l, tr, 0, 1, M, idx, A, ws, ws_bytes, s);
     printf("diag  %8.2f us/launch\n", T.stop(s) * 1e3 / 50);
