@@ -6,10 +6,11 @@
 //   * Its rows live on chip for the whole run: RT rows per thread in VGPRs/AGPRs (x, g, A[, w]),
 //     RL rows in LDS (SoA), the remainder streamed from HBM each step (coalesced, like K2).
 //   * Per step: every block evaluates k(x_i, x_j) for its rows, A_i += 2k, block MINLOC, and
-//     publishes ONE candidate record {A_min, global index, x row, g row, w} into a two-bank record
-//     array; it then signals an arrival counter sharded by blockIdx % 8 (8 counters on separate
-//     128-B lines).  Every block waits until all arrivals of the step are visible, reads all G
-//     records and picks the same winner (np.argmin order) -> next step.  Block 0 writes idx.
+//     publishes ONE record {A_min, index} into a two-bank SoA record array; it then signals an
+//     arrival counter sharded by blockIdx % 8 (8 counters on separate 128-B lines).  Every block
+//     waits until all arrivals of the step are visible (8 lanes poll the 8 shards together), reads
+//     the G records (coalesced), picks the same winner (np.argmin order) and reads the winner's
+//     row from the read-only x / g / w arrays -> next step.  Block 0 writes idx.
 //   * Hand-off form = MI355X_MICROARCH.md "Valid forms", table row 1: payload written by ONE wave
 //     with 8-B agent-scope (sc1) stores, that wave drains vmcnt(0), then ONE lane's agent-scope
 //     atomic add; the consumer polls with sc1 loads, joins a workgroup barrier, reads with sc1 loads.
@@ -80,90 +81,81 @@ struct PersistArgs {
     double l, tr;
     int64_t m;            // n_points
     uint32_t* idx_out;
-    double* recs;         // 2 banks x G records x stride doubles
-    int64_t stride;
+    double* rec_val;      // 2 banks x G: block minima
+    int64_t* rec_idx;     // 2 banks x G: their row indices
     unsigned* counters;   // kShards counters, kShardStride words apart
     unsigned* status;     // [0]: 0 ok, 1 timeout
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
 };
 
-// publish this block's record for step t (bank t & 1) and signal its arrival
-template <int D>
+// publish this block's {A_min, index} for step t (bank t & 1) and signal its arrival
 __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, int64_t li,
                                         int64_t t) {
     p_block_minloc(v, li, sc->v, sc->i);
-    if (threadIdx.x < 64) {   // wave 0 stores the whole record, drains, lane 0 signals
-        double* rec = a.recs + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * a.stride;
-        const int k = threadIdx.x;
-        if (k == 0) st_f64(rec, v);
-        if (k == 1) st_f64(rec + 1, __longlong_as_double((long long)li));
-        if (li != INT64_MAX && k < 2 * D + 1) {
-            double val;
-            if (k < D) val = a.x[(int64_t)k * a.ld + li];
-            else if (k < 2 * D) val = a.g[(int64_t)(k - D) * a.ld + li];
-            else val = a.w ? a.w[li] : 1.0;
-            st_f64(rec + kCandHeader + k, val);
-        }
+    if (threadIdx.x == 0) {   // ONE lane stores the record, drains, signals
+        const int64_t slot = (t & 1) * (int64_t)gridDim.x + blockIdx.x;
+        st_f64(a.rec_val + slot, v);
+        __hip_atomic_store(reinterpret_cast<uint64_t*>(a.rec_idx + slot), (uint64_t)li,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (k == 0)
-            __hip_atomic_fetch_add(a.counters + (blockIdx.x % kShards) * kShardStride, 1u,
-                                   __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_add(a.counters + (blockIdx.x % kShards) * kShardStride, 1u,
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-// wait until every block has published step t, then pick the winner into sc->row.
-// Returns the winner's global index, or -1 if the wait timed out (grid-wide abort).
-template <int D>
+// wait until every block has published step t, reduce the G records (np.argmin order) and stage
+// the winner's row (read-only x, g, w) in sc->row.  Returns the winner's index, -1 on timeout.
+template <int D, bool GF>
 __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
     const int G = gridDim.x;
-    if (threadIdx.x == 0) {
-        int ok = 1;
+    if (threadIdx.x < 64) {   // wave 0: lane s polls shard s; all shards in flight together
+        const int lane = threadIdx.x;
+        const unsigned ns = lane < kShards ? (unsigned)((G - lane + kShards - 1) / kShards) : 0u;
+        const unsigned want = ns * (unsigned)(t + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        for (int s = 0; s < kShards && ok; ++s) {
-            const unsigned ns = (unsigned)((G - s + kShards - 1) / kShards);   // blocks with b % 8 == s
-            const unsigned want = ns * (unsigned)(t + 1);
-            while (__hip_atomic_load(a.counters + s * kShardStride, __ATOMIC_RELAXED,
-                                     __HIP_MEMORY_SCOPE_AGENT) < want) {
-                __builtin_amdgcn_s_sleep(1);
-                if (__builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks ||
-                    __hip_atomic_load(a.status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) {
-                    ok = 0;
-                    break;
-                }
+        int ok = 1;
+        for (unsigned it = 0;; ++it) {
+            const unsigned c = lane < kShards
+                                   ? __hip_atomic_load(a.counters + lane * kShardStride, __ATOMIC_RELAXED,
+                                                       __HIP_MEMORY_SCOPE_AGENT)
+                                   : 0u;
+            if (__all(c >= want)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if ((it & 31) == 31) {
+                const bool late = __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks;
+                const bool other = __hip_atomic_load(a.status, __ATOMIC_RELAXED,
+                                                     __HIP_MEMORY_SCOPE_AGENT) != 0;
+                if (late || other) { ok = 0; break; }
             }
         }
-        if (!ok) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        sc->abort = !ok;
+        if (lane == 0) {
+            if (!ok) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sc->abort = !ok;
+        }
     }
     __syncthreads();
     if (sc->abort) return -1;
-    const double* bank = a.recs + (t & 1) * (int64_t)G * a.stride;
+    const int64_t base = (t & 1) * (int64_t)G;
     double v = INFINITY;
     int64_t gi = INT64_MAX;
-    double row[2 * D + 1];
     for (int r = threadIdx.x; r < G; r += kPBlock) {
-        const double* rec = bank + (int64_t)r * a.stride;
-        double rrow[2 * D + 1];
-        const double rv = ld_f64(rec);
-        const int64_t ri = (int64_t)__double_as_longlong(ld_f64(rec + 1));
-#pragma unroll
-        for (int k = 0; k < 2 * D + 1; ++k) rrow[k] = ld_f64(rec + kCandHeader + k);
-        if (better(rv, ri, v, gi)) {
-            v = rv; gi = ri;
-#pragma unroll
-            for (int k = 0; k < 2 * D + 1; ++k) row[k] = rrow[k];
-        }
+        const double rv = ld_f64(a.rec_val + base + r);
+        const int64_t ri = (int64_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(a.rec_idx + base + r),
+                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (better(rv, ri, v, gi)) { v = rv; gi = ri; }
     }
-    double bv = v;
-    int64_t bi = gi;
-    p_block_minloc(bv, bi, sc->v, sc->i);
-    if (gi == bi && gi != INT64_MAX) {
-#pragma unroll
-        for (int k = 0; k < 2 * D + 1; ++k) sc->row[k] = row[k];
+    p_block_minloc(v, gi, sc->v, sc->i);
+    const int k = threadIdx.x;
+    if (k < 2 * D + (GF ? 1 : 0)) {
+        double val;
+        if (k < D) val = a.x[(int64_t)k * a.ld + gi];
+        else if (k < 2 * D) val = a.g[(int64_t)(k - D) * a.ld + gi];
+        else val = a.w[gi];
+        sc->row[k] = val;
     }
     __syncthreads();
-    return bi;
+    return gi;
 }
 
 template <int D, bool GF, int RT>
@@ -239,18 +231,28 @@ __global__ __launch_bounds__(kPBlock, 1) void greedy_persistent(PersistArgs a) {
         a.A[row] = kv;
         if (better(kv, row, bv, bi)) { bv = kv; bi = row; }
     }
-    publish<D>(a, sc, bv, bi, 0);
+    publish(a, sc, bv, bi, 0);
 
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
     int64_t t = 1;
     for (; t < a.m; ++t) {
-        const int64_t win = wait_and_pick<D>(a, sc, t - 1);
+        const int64_t win = wait_and_pick<D, GF>(a, sc, t - 1);
         if (win < 0) break;
         if (blockIdx.x == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
         double xj[D], gj[D];
 #pragma unroll
         for (int k = 0; k < D; ++k) { xj[k] = sc->row[k]; gj[k] = sc->row[D + k]; }
         const double wj = GF ? sc->row[2 * D] : 1.0;
+        // first streamed row: issue its loads now, they land while the on-chip rows compute
+        int64_t srow = str_base + tid;
+        bool have = srow < r1;
+        double nx[D], ng[D], na = 0.0, nw = 1.0;
+        if (have) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) { nx[k] = a.x[k * ld + srow]; ng[k] = a.g[k * ld + srow]; }
+            na = a.A[srow];
+            if constexpr (GF) nw = a.w[srow];
+        }
         bv = INFINITY;
         bi = INT64_MAX;
 #pragma unroll
@@ -272,21 +274,31 @@ __global__ __launch_bounds__(kPBlock, 1) void greedy_persistent(PersistArgs a) {
             sa[e] = av;
             if (row < r1 && better(av, row, bv, bi)) { bv = av; bi = row; }
         }
-        for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
+        while (have) {   // streamed rows, one row of loads kept in flight ahead of the compute
             double xi[D], gi[D];
 #pragma unroll
-            for (int k = 0; k < D; ++k) { xi[k] = a.x[k * ld + row]; gi[k] = a.g[k * ld + row]; }
+            for (int k = 0; k < D; ++k) { xi[k] = nx[k]; gi[k] = ng[k]; }
+            const double ai = na, wi = nw;
+            const int64_t row = srow;
+            srow += kPBlock;
+            have = srow < r1;
+            if (have) {
+#pragma unroll
+                for (int k = 0; k < D; ++k) { nx[k] = a.x[k * ld + srow]; ng[k] = a.g[k * ld + srow]; }
+                na = a.A[srow];
+                if constexpr (GF) nw = a.w[srow];
+            }
             double kv = pair_value_ct<D>(xi, gi, xj, gj, l, l2, tr);
-            if constexpr (GF) kv = (kv * a.w[row]) * wj;
-            const double av = a.A[row] + 2.0 * kv;
+            if constexpr (GF) kv = (kv * wi) * wj;
+            const double av = ai + 2.0 * kv;
             a.A[row] = av;
             if (better(av, row, bv, bi)) { bv = av; bi = row; }
         }
-        publish<D>(a, sc, bv, bi, t);
+        publish(a, sc, bv, bi, t);
     }
     int64_t done = t;   // idx[0 .. done-1) are written
     if (t == a.m) {
-        const int64_t win = wait_and_pick<D>(a, sc, a.m - 1);
+        const int64_t win = wait_and_pick<D, GF>(a, sc, a.m - 1);
         if (win >= 0) {
             if (blockIdx.x == 0 && tid == 0) a.idx_out[a.m - 1] = (uint32_t)win;
             done = a.m + 1;
@@ -312,8 +324,9 @@ __global__ __launch_bounds__(kPBlock, 1) void greedy_persistent(PersistArgs a) {
 // host side
 // ------------------------------------------------------------------------------------------
 int64_t persistent_ws_bytes(int d, int G) {
-    // [control: counters 8 x 128 B + status 128 B][2 record banks of G records]
-    return kWsControlBytes + 2 * (int64_t)G * cand_stride(d) * 8;
+    // [control: counters 8 x 128 B + status 128 B][2 x G values][2 x G indices]
+    (void)d;
+    return kWsControlBytes + 4 * (int64_t)G * 8;
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
@@ -390,8 +403,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.idx_out = idx_out;
     a.counters = reinterpret_cast<unsigned*>(p);
     a.status = reinterpret_cast<unsigned*>(p + kShards * 128);
-    a.recs = reinterpret_cast<double*>(p + kWsControlBytes);
-    a.stride = cand_stride(d);
+    a.rec_val = reinterpret_cast<double*>(p + kWsControlBytes);
+    a.rec_idx = reinterpret_cast<int64_t*>(p + kWsControlBytes + 2 * (int64_t)G * 8);
     a.rows_per_block = R;
     a.RL = (int)RL;
     hipError_t e = hipMemsetAsync(p, 0, kWsControlBytes, s);
