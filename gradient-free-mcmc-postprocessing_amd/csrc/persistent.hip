@@ -6,14 +6,11 @@
 //   * Its rows live on chip for the whole run: RT rows per thread in VGPRs/AGPRs (x, g, A[, w]),
 //     RL rows in LDS (SoA), the remainder streamed from HBM each step (coalesced, like K2).
 //   * Per step: every block evaluates k(x_i, x_j) for its rows, A_i += 2k, block MINLOC, and
-//     publishes ONE record {A_min, index} into a two-bank SoA record array; it then signals an
-//     arrival counter sharded by blockIdx % 8 (8 counters on separate 128-B lines).  Every block
-//     waits until all arrivals of the step are visible (8 lanes poll the 8 shards together), reads
-//     the G records (coalesced), picks the same winner (np.argmin order) and reads the winner's
-//     row from the read-only x / g / w arrays -> next step.  Block 0 writes idx.
-//   * Hand-off form = MI355X_MICROARCH.md "Valid forms", table row 1: payload written by ONE wave
-//     with 8-B agent-scope (sc1) stores, that wave drains vmcnt(0), then ONE lane's agent-scope
-//     atomic add; the consumer polls with sc1 loads, joins a workgroup barrier, reads with sc1 loads.
+//     publishes ONE record {A_min, index} as three data-tagged 8-byte granules (tag = step + 1;
+//     MI355X_MICROARCH.md recipe R2, "the data IS the flag": no fence, no counter).  One wave per
+//     block sweeps all G records until every tag matches, reduces them (np.argmin order) and the
+//     block reads the winner's row from the read-only x / g / w arrays -> next step.  Block 0
+//     writes idx.  Two record banks alternate by step parity.
 //   * Every spin is bounded by a wall-clock timeout (s_memrealtime); a timeout sets status[0] and
 //     every block leaves the step loop, so the grid always drains.
 // Arithmetic per pair: identical to K2 (stein_math.hpp), so results are bit-identical to st_greedy's
@@ -28,18 +25,8 @@ namespace {
 constexpr int kPBlock = 256;
 constexpr int kPWaves = kPBlock / 64;
 constexpr int kShards = 8;
-constexpr int kShardStride = 32;            // u32 words between counters (128 B)
+constexpr int kMaxGrid = 256;               // one block per CU on MI355X (256 CUs)
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
-
-__device__ __forceinline__ void st_f64(double* p, double v) {
-    __hip_atomic_store(reinterpret_cast<uint64_t*>(p), (uint64_t)__double_as_longlong(v),
-                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ double ld_f64(const double* p) {
-    return __longlong_as_double((long long)__hip_atomic_load(reinterpret_cast<const uint64_t*>(p),
-                                                             __ATOMIC_RELAXED,
-                                                             __HIP_MEMORY_SCOPE_AGENT));
-}
 
 __device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) {
 #pragma unroll
@@ -81,71 +68,84 @@ struct PersistArgs {
     double l, tr;
     int64_t m;            // n_points
     uint32_t* idx_out;
-    double* rec_val;      // 2 banks x G: block minima
-    int64_t* rec_idx;     // 2 banks x G: their row indices
-    unsigned* counters;   // kShards counters, kShardStride words apart
+    uint64_t* gran;       // 2 banks x G records x 4 granules (3 used)
     unsigned* status;     // [0]: 0 ok, 1 timeout
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
 };
 
-// publish this block's {A_min, index} for step t (bank t & 1) and signal its arrival
+// Exchange = self-validating granules (MI355X_MICROARCH.md R2: "the data IS the flag"): each block
+// publishes {A_min, index} for step t as three 8-byte granules {tag = t+1 : 32-bit payload}
+// (value low word, value high word, index), each written by ONE aligned 8-B agent-scope store.
+// A consumer accepts a record only when all three tags equal t+1; banks alternate by step parity.
 __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, int64_t li,
                                         int64_t t) {
     p_block_minloc(v, li, sc->v, sc->i);
-    if (threadIdx.x == 0) {   // ONE lane stores the record, drains, signals
-        const int64_t slot = (t & 1) * (int64_t)gridDim.x + blockIdx.x;
-        st_f64(a.rec_val + slot, v);
-        __hip_atomic_store(reinterpret_cast<uint64_t*>(a.rec_idx + slot), (uint64_t)li,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_fetch_add(a.counters + (blockIdx.x % kShards) * kShardStride, 1u,
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x == 0) {
+        uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * 4;
+        const uint64_t tag = (uint64_t)(uint32_t)(t + 1) << 32;
+        const uint64_t vb = (uint64_t)__double_as_longlong(v);
+        const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
+        __hip_atomic_store(gr + 0, tag | (vb & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gr + 1, tag | (vb >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gr + 2, tag | ib, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-// wait until every block has published step t, reduce the G records (np.argmin order) and stage
-// the winner's row (read-only x, g, w) in sc->row.  Returns the winner's index, -1 on timeout.
+// wave 0 sweeps the G records of step t until every tag is t+1 (bounded), reduces them
+// (np.argmin order); then the winner's row is read from the read-only x / g / w arrays into
+// sc->row.  Returns the winner's index, or -1 if the sweep timed out (grid-wide abort).
 template <int D, bool GF>
 __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
     const int G = gridDim.x;
-    if (threadIdx.x < 64) {   // wave 0: lane s polls shard s; all shards in flight together
+    if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const unsigned ns = lane < kShards ? (unsigned)((G - lane + kShards - 1) / kShards) : 0u;
-        const unsigned want = ns * (unsigned)(t + 1);
+        const uint64_t* bank = a.gran + (t & 1) * (int64_t)G * 4;
+        const uint32_t want = (uint32_t)(t + 1);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-        int ok = 1;
+        double v = INFINITY;
+        int64_t gi = INT64_MAX;
+        int ok_all = 1;
         for (unsigned it = 0;; ++it) {
-            const unsigned c = lane < kShards
-                                   ? __hip_atomic_load(a.counters + lane * kShardStride, __ATOMIC_RELAXED,
-                                                       __HIP_MEMORY_SCOPE_AGENT)
-                                   : 0u;
-            if (__all(c >= want)) break;
+            bool ok = true;
+            v = INFINITY;
+            gi = INT64_MAX;
+#pragma unroll
+            for (int c = 0; c < kMaxGrid / 64; ++c) {
+                const int r = lane + 64 * c;
+                if (r < G) {
+                    const uint64_t* gr = bank + (int64_t)r * 4;
+                    const uint64_t g0 = __hip_atomic_load(gr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t g1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t g2 = __hip_atomic_load(gr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    ok &= ((uint32_t)(g0 >> 32) == want) & ((uint32_t)(g1 >> 32) == want) &
+                          ((uint32_t)(g2 >> 32) == want);
+                    const double rv = __longlong_as_double(
+                        (long long)((g1 << 32) | (g0 & 0xFFFFFFFFull)));
+                    const uint32_t ib = (uint32_t)g2;
+                    const int64_t ri = ib == 0xFFFFFFFFu ? INT64_MAX : (int64_t)ib;
+                    if (better(rv, ri, v, gi)) { v = rv; gi = ri; }
+                }
+            }
+            if (__all(ok)) break;
             __builtin_amdgcn_s_sleep(1);
-            if ((it & 31) == 31) {
+            if ((it & 15) == 15) {
                 const bool late = __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks;
                 const bool other = __hip_atomic_load(a.status, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT) != 0;
-                if (late || other) { ok = 0; break; }
+                if (__any(late || other)) { ok_all = 0; break; }
             }
         }
+        p_wave_minloc(v, gi);
         if (lane == 0) {
-            if (!ok) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            sc->abort = !ok;
+            if (!ok_all) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            sc->abort = !ok_all;
+            sc->i[0] = gi;
         }
     }
     __syncthreads();
     if (sc->abort) return -1;
-    const int64_t base = (t & 1) * (int64_t)G;
-    double v = INFINITY;
-    int64_t gi = INT64_MAX;
-    for (int r = threadIdx.x; r < G; r += kPBlock) {
-        const double rv = ld_f64(a.rec_val + base + r);
-        const int64_t ri = (int64_t)__hip_atomic_load(reinterpret_cast<const uint64_t*>(a.rec_idx + base + r),
-                                                      __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (better(rv, ri, v, gi)) { v = rv; gi = ri; }
-    }
-    p_block_minloc(v, gi, sc->v, sc->i);
+    const int64_t gi = sc->i[0];
     const int k = threadIdx.x;
     if (k < 2 * D + (GF ? 1 : 0)) {
         double val;
@@ -324,9 +324,9 @@ __global__ __launch_bounds__(kPBlock, 1) void greedy_persistent(PersistArgs a) {
 // host side
 // ------------------------------------------------------------------------------------------
 int64_t persistent_ws_bytes(int d, int G) {
-    // [control: counters 8 x 128 B + status 128 B][2 x G values][2 x G indices]
+    // [control: status (and reserved) words][2 banks x G records x 4 granules of 8 B]
     (void)d;
-    return kWsControlBytes + 4 * (int64_t)G * 8;
+    return kWsControlBytes + 2 * (int64_t)G * 4 * 8;
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
@@ -363,7 +363,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
                                     int* used) {
     *used = 0;
-    if (g_persist_rt == 0 || (d != 2 && d != 4) || m < 1) return hipErrorNotSupported;
+    if (g_persist_rt == 0 || (d != 2 && d != 4) || m < 1 || m >= 0xFFFFFFFFll || n >= 0xFFFFFFFFll)
+        return hipErrorNotSupported;
     int dev = 0, cus = 0, lds_max = 0, lds_optin = 0, coop = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -376,7 +377,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         lds_optin > lds_max)
         lds_max = lds_optin;
     if (lds_max > 163840) lds_max = 163840;
-    int G = cus > kMaxBlocks ? kMaxBlocks : cus;
+    int G = cus > kMaxGrid ? kMaxGrid : cus;
     const int64_t min_rows = 256;   // fewer blocks for small n: exchange cost grows with G
     if (n < (int64_t)G * min_rows) G = (int)((n + min_rows - 1) / min_rows);
     if (G < 1) G = 1;
@@ -401,13 +402,12 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.x = x; a.g = g; a.w = w; a.A = A;
     a.n = n; a.ld = ld; a.l = l; a.tr = tr; a.m = m;
     a.idx_out = idx_out;
-    a.counters = reinterpret_cast<unsigned*>(p);
     a.status = reinterpret_cast<unsigned*>(p + kShards * 128);
-    a.rec_val = reinterpret_cast<double*>(p + kWsControlBytes);
-    a.rec_idx = reinterpret_cast<int64_t*>(p + kWsControlBytes + 2 * (int64_t)G * 8);
+    a.gran = reinterpret_cast<uint64_t*>(p + kWsControlBytes);
     a.rows_per_block = R;
     a.RL = (int)RL;
-    hipError_t e = hipMemsetAsync(p, 0, kWsControlBytes, s);
+    // zero status and every granule tag (a stale tag from a previous run must never match)
+    hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G), s);
     if (e != hipSuccess) return e;
     if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, G, lds, s) : launch_p_rt<2, false>(a, rt, G, lds, s);
     else e = gf ? launch_p_rt<4, true>(a, rt, G, lds, s) : launch_p_rt<4, false>(a, rt, G, lds, s);

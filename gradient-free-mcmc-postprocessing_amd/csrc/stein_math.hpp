@@ -17,21 +17,23 @@
 
 namespace st {
 
-// correctly rounded (to ~2^-100) qf^1.5 and qf^2.5 from s = sqrt(qf) and its exact residual
+// qf^1.5 and qf^2.5 correctly rounded to ~2^-100 (then rounded once), from s = sqrt(qf) (correctly
+// rounded) and its exact residual e = qf - s^2 (fma).  sqrt(qf) = s + e/(2s) + O(2^-106 s), and the
+// correction terms q * e/(2s) and q^2 * e/(2s) equal (s/2) e and (q s/2) e to 2^-53 relative of a term
+// that is itself ~2^-53 of the result -- so no division is needed.
 __device__ __forceinline__ void pow_15_25(double q, double& p15, double& p25, double& s) {
     s = __builtin_sqrt(q);
     const double e = __builtin_fma(-s, s, q);
-    const double c = e / (2.0 * s);
     const double hi = q * s;
     double lo = __builtin_fma(q, s, -hi);
-    lo = __builtin_fma(q, c, lo);
+    lo = __builtin_fma(0.5 * s, e, lo);
     p15 = hi + lo;
     const double q2 = q * q;
     const double q2lo = __builtin_fma(q, q, -q2);
     const double hi2 = q2 * s;
     double lo2 = __builtin_fma(q2, s, -hi2);
-    lo2 = __builtin_fma(q2, c, lo2);
     lo2 = __builtin_fma(q2lo, s, lo2);
+    lo2 = __builtin_fma(0.5 * hi, e, lo2);
     p25 = hi2 + lo2;
 }
 
@@ -173,11 +175,14 @@ __device__ __forceinline__ double diag_value_rt(const double* __restrict__ gi_co
     return finish_pair(0.0, 0.0, 0.0, t3s, tr);
 }
 
-// np.argmin order: NaN is the minimum (first NaN wins), otherwise smaller value, ties -> lower index
+// np.argmin order: NaN is the minimum (first NaN wins), otherwise smaller value, ties -> lower index.
+// Branch-free (selects, no exec-mask branches in the per-candidate hot loop).
 __device__ __forceinline__ bool better(double a, int64_t ia, double b, int64_t ib) {
     const bool na = __builtin_isnan(a), nb = __builtin_isnan(b);
-    if (na | nb) return na && (!nb || ia < ib);
-    return (a < b) || (a == b && ia < ib);
+    const bool il = ia < ib;
+    const bool num = (a < b) | ((a == b) & il);
+    const bool nan = na & (!nb | il);
+    return (na | nb) ? nan : num;
 }
 
 }  // namespace st

@@ -51,21 +51,22 @@ static double pairwise_sum(const double *v, int64_t n) {
     }
 }
 
-/* correctly rounded qf^1.5, qf^2.5 via s = sqrt(qf) and its exact residual */
+/* correctly rounded (to ~2^-100, then rounded once) qf^1.5, qf^2.5 from s = sqrt(qf) and its exact
+ * residual e = qf - s^2: the correction terms q*e/(2s), q^2*e/(2s) are evaluated as (s/2)*e and
+ * (q*s/2)*e (equal to 2^-53 relative of a 2^-53-relative term) -- the kernels' exact op sequence */
 static void pow_15_25(double q, double *p15, double *p25, double *sq) {
     double s = sqrt(q);
     double e = fma(-s, s, q);
-    double c = e / (2.0 * s);
     double hi = q * s;
     double lo = fma(q, s, -hi);
-    lo = fma(q, c, lo);
+    lo = fma(0.5 * s, e, lo);
     *p15 = hi + lo;
     double q2 = q * q;
     double q2lo = fma(q, q, -q2);
     double hi2 = q2 * s;
     double lo2 = fma(q2, s, -hi2);
-    lo2 = fma(q2, c, lo2);
     lo2 = fma(q2lo, s, lo2);
+    lo2 = fma(0.5 * hi, e, lo2);
     *p25 = hi2 + lo2;
     *sq = s;
 }
