@@ -24,14 +24,7 @@ namespace st {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 
-__device__ __forceinline__ void wave_minloc(double& v, int64_t& i) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double ov = __shfl_xor(v, off, 64);
-        const int64_t oi = __shfl_xor(i, off, 64);
-        if (better(ov, oi, v, i)) { v = ov; i = oi; }
-    }
-}
+__device__ __forceinline__ void wave_minloc(double& v, int64_t& i) { wave_minloc_dpp(v, i); }
 
 // Block-wide MINLOC; result valid in every thread.
 __device__ __forceinline__ void block_minloc(double& v, int64_t& i, double* s_v, int64_t* s_i) {

@@ -28,14 +28,7 @@ constexpr int kShards = 8;
 constexpr int kMaxGrid = 256;               // one block per CU on MI355X (256 CUs)
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
 
-__device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) {
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-        const double ov = __shfl_xor(v, off, 64);
-        const int64_t oi = __shfl_xor(i, off, 64);
-        if (better(ov, oi, v, i)) { v = ov; i = oi; }
-    }
-}
+__device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minloc_dpp(v, i); }
 
 __device__ __forceinline__ void p_block_minloc(double& v, int64_t& i, double* s_v, int64_t* s_i) {
     p_wave_minloc(v, i);
