@@ -22,30 +22,17 @@ namespace st {
 
 namespace {
 
-constexpr int kPBlock = 256;
-constexpr int kPWaves = kPBlock / 64;
+constexpr int kMaxPWaves = 8;                // up to 512-thread blocks
 constexpr int kShards = 8;
 constexpr int kMaxGrid = 256;               // one block per CU on MI355X (256 CUs)
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
 
 __device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minloc_dpp(v, i); }
 
-__device__ __forceinline__ void p_block_minloc(double& v, int64_t& i, double* s_v, int64_t* s_i) {
-    p_wave_minloc(v, i);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) { s_v[wave] = v; s_i[wave] = i; }
-    __syncthreads();
-    v = s_v[0]; i = s_i[0];
-#pragma unroll
-    for (int w = 1; w < kPWaves; ++w)
-        if (better(s_v[w], s_i[w], v, i)) { v = s_v[w]; i = s_i[w]; }
-    __syncthreads();
-}
-
 struct Scratch {          // small per-block scratch at the start of the dynamic LDS region
     double row[2 * kMaxCtDim + 2];
-    double v[kPWaves];
-    int64_t i[kPWaves];
+    double v[kMaxPWaves];
+    int64_t i[kMaxPWaves];
     int abort;
     int pad[3];
 };
@@ -65,16 +52,40 @@ struct PersistArgs {
     unsigned* status;     // [0]: 0 ok, 1 timeout
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
+    uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
 };
+
+// Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
+// every block records s_memrealtime (100 MHz, chip-wide clock) at each phase of steps
+// [kStampFirst, kStampFirst + kStampSteps).
+[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 6;
+#ifdef ST_PERSIST_STAMPS
+#define ST_STAMP(a, t, ph)                                                                         \
+    do {                                                                                            \
+        if ((a).stamps && threadIdx.x == 0 && (t) >= kStampFirst && (t) < kStampFirst + kStampSteps) \
+            (a).stamps[((int64_t)blockIdx.x * kStampSteps + ((t) - kStampFirst)) * kStampPhases + (ph)] = \
+                __builtin_amdgcn_s_memrealtime();                                                    \
+    } while (0)
+#else
+#define ST_STAMP(a, t, ph) do { } while (0)
+#endif
 
 // Exchange = self-validating granules (MI355X_MICROARCH.md R2: "the data IS the flag"): each block
 // publishes {A_min, index} for step t as three 8-byte granules {tag = t+1 : 32-bit payload}
 // (value low word, value high word, index), each written by ONE aligned 8-B agent-scope store.
 // A consumer accepts a record only when all three tags equal t+1; banks alternate by step parity.
+template <int NT>
 __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, int64_t li,
                                         int64_t t) {
-    p_block_minloc(v, li, sc->v, sc->i);
-    if (threadIdx.x == 0) {
+    p_wave_minloc(v, li);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    if (lane == 0) { sc->v[wave] = v; sc->i[wave] = li; }
+    __syncthreads();
+    if (threadIdx.x == 0) {   // ONE lane combines the wave minima and stores the three granules
+        v = sc->v[0];
+        li = sc->i[0];
+#pragma unroll
+        for (int w = 1; w < NT / 64; ++w) take_if_better(sc->v[w], sc->i[w], v, li);
         uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * 4;
         const uint64_t tag = (uint64_t)(uint32_t)(t + 1) << 32;
         const uint64_t vb = (uint64_t)__double_as_longlong(v);
@@ -91,6 +102,7 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 template <int D, bool GF>
 __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
     const int G = gridDim.x;
+    ST_STAMP(a, t + 1, 0);
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
         const uint64_t* bank = a.gran + (t & 1) * (int64_t)G * 4;
@@ -129,6 +141,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                 if (__any(late || other)) { ok_all = 0; break; }
             }
         }
+        ST_STAMP(a, t + 1, 1);
         p_wave_minloc(v, gi);
         if (lane == 0) {
             if (!ok_all) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -148,11 +161,13 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         sc->row[k] = val;
     }
     __syncthreads();
+    ST_STAMP(a, t + 1, 2);
     return gi;
 }
 
-template <int D, bool GF, int RT>
-__global__ __launch_bounds__(kPBlock, 1) void greedy_persistent(PersistArgs a) {
+template <int D, bool GF, int RT, int NT>
+__global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
+    constexpr int kPBlock = NT;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     Scratch* sc = reinterpret_cast<Scratch*>(lds);
     const int RL = a.RL;
@@ -224,7 +239,7 @@ __global__ __launch_bounds__(kPBlock, 1) void greedy_persistent(PersistArgs a) {
         a.A[row] = kv;
         if (better(kv, row, bv, bi)) { bv = kv; bi = row; }
     }
-    publish(a, sc, bv, bi, 0);
+    publish<NT>(a, sc, bv, bi, 0);
 
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
     int64_t t = 1;
@@ -287,7 +302,9 @@ __global__ __launch_bounds__(kPBlock, 1) void greedy_persistent(PersistArgs a) {
             a.A[row] = av;
             if (better(av, row, bv, bi)) { bv = av; bi = row; }
         }
-        publish(a, sc, bv, bi, t);
+        ST_STAMP(a, t, 3);
+        publish<NT>(a, sc, bv, bi, t);
+        ST_STAMP(a, t, 4);
     }
     int64_t done = t;   // idx[0 .. done-1) are written
     if (t == a.m) {
@@ -323,30 +340,47 @@ int64_t persistent_ws_bytes(int d, int G) {
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
-int persistent_tune(int value) {
-    if (value < -1 || value > 64) return -1;
-    g_persist_rt = value;
-    return 0;
+static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (512)
+static uint64_t* g_stamps = nullptr;
+#ifdef ST_PERSIST_STAMPS
+extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
+#endif
+int persistent_tune(int key, int value) {
+    if (key == 3) {
+        if (value < -1 || value > 64) return -1;
+        g_persist_rt = value;
+        return 0;
+    }
+    if (key == 4) {
+        if (value != -1 && value != 256 && value != 512) return -1;
+        g_persist_nt = value;
+        return 0;
+    }
+    return -1;
 }
 
-template <int D, bool GF, int RT>
+template <int D, bool GF, int RT, int NT>
 static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s) {
-    auto fn = greedy_persistent<D, GF, RT>;
+    auto fn = greedy_persistent<D, GF, RT, NT>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     PersistArgs args = a;
     void* kargs[] = {&args};
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(kPBlock),
-                                      kargs, lds, s);
+    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs,
+                                      lds, s);
 }
 
 template <int D, bool GF>
-static hipError_t launch_p_rt(const PersistArgs& a, int rt, int G, size_t lds, hipStream_t s) {
+static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int G, size_t lds, hipStream_t s) {
+    if (nt == 512) {
+        if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s);
+        return launch_p<D, GF, 8, 512>(a, G, lds, s);
+    }
     switch (rt) {
-        case 4: return launch_p<D, GF, 4>(a, G, lds, s);
-        case 8: return launch_p<D, GF, 8>(a, G, lds, s);
-        default: return launch_p<D, GF, 16>(a, G, lds, s);
+        case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s);
+        case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s);
+        default: return launch_p<D, GF, 16, 256>(a, G, lds, s);
     }
 }
 
@@ -376,15 +410,18 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     if (G < 1) G = 1;
     if (persistent_ws_bytes(d, G) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n + G - 1) / G;
-    int rt = g_persist_rt > 0 ? g_persist_rt : 16;
-    if (rt != 4 && rt != 8 && rt != 16) rt = 16;
-    while (rt > 4 && (int64_t)rt * kPBlock > R) rt /= 2;   // do not hold empty register rows
+    const int nt = g_persist_nt > 0 ? g_persist_nt : 512;
+    const int rt_max = nt == 512 ? 8 : 16;
+    int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
+    if (rt != 4 && rt != 8 && rt != 16) rt = rt_max;
+    if (rt > rt_max) rt = rt_max;
+    while (rt > 4 && (int64_t)rt * nt > R) rt /= 2;   // do not hold empty register rows
     const bool gf = w != nullptr;
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);
     const size_t head = (sizeof(Scratch) + 15) / 16 * 16;
     const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) - 1024;   // static + slack
     int64_t RL = (int64_t)((budget - head) / row_bytes);
-    const int64_t need = R - (int64_t)rt * kPBlock;
+    const int64_t need = R - (int64_t)rt * nt;
     if (RL > need) RL = need > 0 ? need : 0;
     RL = RL / 64 * 64;
     if (RL < 0) RL = 0;
@@ -399,11 +436,12 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.gran = reinterpret_cast<uint64_t*>(p + kWsControlBytes);
     a.rows_per_block = R;
     a.RL = (int)RL;
+    a.stamps = g_stamps;
     // zero status and every granule tag (a stale tag from a previous run must never match)
     hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G), s);
     if (e != hipSuccess) return e;
-    if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, G, lds, s) : launch_p_rt<2, false>(a, rt, G, lds, s);
-    else e = gf ? launch_p_rt<4, true>(a, rt, G, lds, s) : launch_p_rt<4, false>(a, rt, G, lds, s);
+    if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, nt, G, lds, s) : launch_p_rt<2, false>(a, rt, nt, G, lds, s);
+    else e = gf ? launch_p_rt<4, true>(a, rt, nt, G, lds, s) : launch_p_rt<4, false>(a, rt, nt, G, lds, s);
     if (e == hipSuccess) *used = 1;
     return e;
 }

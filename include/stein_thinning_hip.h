@@ -56,7 +56,8 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * measured best on MI355X): key 0 = grid cap (blocks, 1..1024), key 1 = candidates per lane
  * (1, 2, 4; d = 2 and 4 kernels; -1 = automatic), key 2 = register prefetch of the next tile
  * (0/1; -1 = automatic), key 3 = persistent kernel register rows per thread (4, 8, 16;
- * -1 = automatic, 0 = disable the persistent kernel).
+ * -1 = automatic, 0 = disable the persistent kernel), key 4 = persistent kernel threads per
+ * block (256, 512; -1 = automatic).
  */
 int st_tune(int32_t key, int32_t value);
 

@@ -12,6 +12,10 @@
 
 #include "../include/stein_thinning_hip.h"
 
+#ifdef ST_PERSIST_STAMPS
+extern "C" int st_debug_set_stamps(uint64_t* buf);
+#endif
+
 #define CK(x)                                                                   \
     do {                                                                        \
         hipError_t e_ = (x);                                                    \
@@ -157,8 +161,11 @@ int main(int argc, char** argv) {
     }
     st_tune(0, 256); st_tune(1, -1); st_tune(2, -1);
     // whole-run st_greedy: persistent kernel (register rows per thread rt; 0 = launch per step)
-    for (int rt : {16, 8, 4, 0}) {
+    struct V { int rt, nt; };
+    for (V cfg : {V{8, 512}, V{4, 512}, V{16, 256}, V{8, 256}, V{0, 256}}) {
+        const int rt = cfg.rt;
         st_tune(3, rt);
+        st_tune(4, cfg.nt);
         for (int rep = 0; rep < 3; ++rep) {
             T.start(s);
             int rc = st_greedy(x, g, nullptr, n, d, ld, l, tr, M, idx, A, ws, ws_bytes, s);
@@ -167,11 +174,59 @@ int main(int argc, char** argv) {
             std::vector<uint32_t> h(M);
             CK(hipMemcpy(h.data(), idx, 4 * M, hipMemcpyDeviceToHost));
             const uint32_t mx = *std::max_element(h.begin(), h.end());
-            printf("st_greedy rt=%2d m=%d  %8.3f ms  %8.2f us/step  idx[0..2]=%u %u %u  max=%u%s\n", rt, M, ms,
+            printf("st_greedy nt=%d rt=%2d m=%d  %8.3f ms  %8.2f us/step  idx[0..2]=%u %u %u  max=%u%s\n", cfg.nt, rt, M, ms,
                    ms * 1e3 / M, h[0], h[1], h[2], mx, mx >= n ? "  POISONED" : "");
+            (void)0;
         }
     }
     st_tune(3, -1);
+    st_tune(4, -1);
+#ifdef ST_PERSIST_STAMPS
+    {   // phase breakdown of persistent steps 20..51 (s_memrealtime, 10 ns ticks)
+        const int SP = 32, PH = 6, GMAX = 256;
+        uint64_t* dst;
+        CK(hipMalloc(&dst, sizeof(uint64_t) * GMAX * SP * PH));
+        CK(hipMemset(dst, 0, sizeof(uint64_t) * GMAX * SP * PH));
+        st_debug_set_stamps(dst);
+        st_greedy(x, g, nullptr, n, d, ld, l, tr, M, idx, A, ws, ws_bytes, s);
+        CK(hipStreamSynchronize(s));
+        st_debug_set_stamps(nullptr);
+        std::vector<uint64_t> h(GMAX * SP * PH);
+        CK(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
+        int G = 0;
+        while (G < GMAX && h[(size_t)G * SP * PH + 0] != 0) ++G;
+        double acc[8] = {0};
+        int cnt = 0;
+        for (int st = 1; st + 1 < SP; ++st) {   // step st: compute (2->3), publish (3->4), exchange
+            uint64_t last_pub = 0, first_start = ~(uint64_t)0, last_start = 0;
+            double c_avg = 0, wait_avg = 0, row_avg = 0, pub_avg = 0;
+            for (int b = 0; b < G; ++b) {
+                const uint64_t* q = &h[((size_t)b * SP + st) * PH];
+                last_pub = std::max<uint64_t>(last_pub, q[4]);
+                c_avg += (double)(q[3] - q[2]);
+                pub_avg += (double)(q[4] - q[3]);
+                const uint64_t* nx = &h[((size_t)b * SP + st + 1) * PH];
+                wait_avg += (double)(nx[1] - nx[0]);
+                row_avg += (double)(nx[2] - nx[1]);
+                first_start = std::min<uint64_t>(first_start, nx[2]);
+                last_start = std::max<uint64_t>(last_start, nx[2]);
+            }
+            acc[0] += c_avg / G; acc[1] += pub_avg / G; acc[2] += wait_avg / G; acc[3] += row_avg / G;
+            acc[4] += (double)(first_start - last_pub); acc[5] += (double)(last_start - first_start);
+            uint64_t s0 = ~(uint64_t)0, s1 = ~(uint64_t)0;
+            for (int b = 0; b < G; ++b) {
+                s0 = std::min<uint64_t>(s0, h[((size_t)b * SP + st) * PH + 2]);
+                s1 = std::min<uint64_t>(s1, h[((size_t)b * SP + st + 1) * PH + 2]);
+            }
+            acc[6] += (double)(s1 - s0);
+            ++cnt;
+        }
+        printf("stamps G=%d (us): compute %.2f  publish %.2f  sweep-wait %.2f  winner-row %.2f  "
+               "last-publish->first-next-start %.2f  start-skew %.2f  step period %.2f\n", G,
+               acc[0] / cnt / 100, acc[1] / cnt / 100, acc[2] / cnt / 100, acc[3] / cnt / 100,
+               acc[4] / cnt / 100, acc[5] / cnt / 100, acc[6] / cnt / 100);
+    }
+#endif
     T.start(s);
     for (int r = 0; r < 50; ++r) st_greedy_steps(x, g, nullptr, n, d, ld, l, tr, 0, 1, M, idx, A, ws, ws_bytes, s);
     printf("diag  %8.2f us/launch\n", T.stop(s) * 1e3 / 50);
