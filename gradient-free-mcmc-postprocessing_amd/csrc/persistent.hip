@@ -37,6 +37,16 @@ struct Scratch {          // small per-block scratch at the start of the dynamic
     int pad[3];
 };
 
+// Per-thread argmin scan: every thread visits its rows in increasing index order, so a candidate
+// replaces the running best only if strictly smaller, or NaN over non-NaN (np.argmin order
+// restricted to increasing indices: ties and later NaNs keep the earlier row).  The running best
+// starts at the thread's first row.  Branch-free; 32-bit row indices (n < 2^32 - 1).
+__device__ __forceinline__ void scan_take(double a, uint32_t ia, double& b, uint32_t& ib) {
+    const bool take = (a < b) | (__builtin_isnan(a) & !__builtin_isnan(b));
+    b = take ? a : b;
+    ib = take ? ia : ib;
+}
+
 }  // namespace
 
 struct PersistArgs {
@@ -75,8 +85,9 @@ struct PersistArgs {
 // (value low word, value high word, index), each written by ONE aligned 8-B agent-scope store.
 // A consumer accepts a record only when all three tags equal t+1; banks alternate by step parity.
 template <int NT>
-__device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, int64_t li,
+__device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, uint32_t row,
                                         int64_t t) {
+    int64_t li = (int64_t)row;   // rows >= n (padding) carry +inf and never win
     p_wave_minloc(v, li);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) { sc->v[wave] = v; sc->i[wave] = li; }
@@ -210,15 +221,18 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
     __syncthreads();
 
     // ---- step 0: diagonal --------------------------------------------------------------------
+    // running best of this thread: starts at its first row (register row 0, which precedes all its
+    // other rows); an out-of-range row contributes +inf with its (>= n) index and never wins
     double bv = INFINITY;
-    int64_t bi = INT64_MAX;
+    uint32_t bi = (uint32_t)(r0 + tid);
 #pragma unroll
     for (int q = 0; q < RT; ++q) {
         const int64_t row = r0 + (int64_t)q * kPBlock + tid;
         double kv = diag_value_ct<D>(gr[q], tr);
         if constexpr (GF) kv = (kv * wr[q]) * wr[q];
         ar[q] = kv;
-        if (row < r1 && better(kv, row, bv, bi)) { bv = kv; bi = row; }
+        const double cand = row < r1 ? kv : INFINITY;
+        if (q == 0) { bv = cand; bi = (uint32_t)row; } else scan_take(cand, (uint32_t)row, bv, bi);
     }
     for (int e = tid; e < RL; e += kPBlock) {
         const int64_t row = lds_base + e;
@@ -228,7 +242,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         double kv = diag_value_ct<D>(gi, tr);
         if constexpr (GF) kv = (kv * sw[e]) * sw[e];
         sa[e] = kv;
-        if (row < r1 && better(kv, row, bv, bi)) { bv = kv; bi = row; }
+        scan_take(row < r1 ? kv : INFINITY, (uint32_t)row, bv, bi);
     }
     for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
         double gi[D];
@@ -237,7 +251,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         double kv = diag_value_ct<D>(gi, tr);
         if constexpr (GF) kv = (kv * a.w[row]) * a.w[row];
         a.A[row] = kv;
-        if (better(kv, row, bv, bi)) { bv = kv; bi = row; }
+        scan_take(kv, (uint32_t)row, bv, bi);
     }
     publish<NT>(a, sc, bv, bi, 0);
 
@@ -261,15 +275,14 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
             na = a.A[srow];
             if constexpr (GF) nw = a.w[srow];
         }
-        bv = INFINITY;
-        bi = INT64_MAX;
 #pragma unroll
         for (int q = 0; q < RT; ++q) {
             const int64_t row = r0 + (int64_t)q * kPBlock + tid;
             double kv = pair_value_ct<D>(xr[q], gr[q], xj, gj, l, l2, tr);
             if constexpr (GF) kv = (kv * wr[q]) * wj;
             ar[q] = ar[q] + 2.0 * kv;
-            if (row < r1 && better(ar[q], row, bv, bi)) { bv = ar[q]; bi = row; }
+            const double cand = row < r1 ? ar[q] : INFINITY;
+            if (q == 0) { bv = cand; bi = (uint32_t)row; } else scan_take(cand, (uint32_t)row, bv, bi);
         }
         for (int e = tid; e < RL; e += kPBlock) {
             const int64_t row = lds_base + e;
@@ -280,7 +293,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
             if constexpr (GF) kv = (kv * sw[e]) * wj;
             const double av = sa[e] + 2.0 * kv;
             sa[e] = av;
-            if (row < r1 && better(av, row, bv, bi)) { bv = av; bi = row; }
+            scan_take(row < r1 ? av : INFINITY, (uint32_t)row, bv, bi);
         }
         while (have) {   // streamed rows, one row of loads kept in flight ahead of the compute
             double xi[D], gi[D];
@@ -300,7 +313,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
             if constexpr (GF) kv = (kv * wi) * wj;
             const double av = ai + 2.0 * kv;
             a.A[row] = av;
-            if (better(av, row, bv, bi)) { bv = av; bi = row; }
+            scan_take(av, (uint32_t)row, bv, bi);
         }
         ST_STAMP(a, t, 3);
         publish<NT>(a, sc, bv, bi, t);
@@ -340,7 +353,7 @@ int64_t persistent_ws_bytes(int d, int G) {
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
-static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (512)
+static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (256)
 static uint64_t* g_stamps = nullptr;
 #ifdef ST_PERSIST_STAMPS
 extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
@@ -410,7 +423,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     if (G < 1) G = 1;
     if (persistent_ws_bytes(d, G) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n + G - 1) / G;
-    const int nt = g_persist_nt > 0 ? g_persist_nt : 512;
+    const int nt = g_persist_nt > 0 ? g_persist_nt : 256;
     const int rt_max = nt == 512 ? 8 : 16;
     int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
     if (rt != 4 && rt != 8 && rt != 16) rt = rt_max;
