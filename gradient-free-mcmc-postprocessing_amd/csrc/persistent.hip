@@ -15,6 +15,8 @@
 //     every block leaves the step loop, so the grid always drains.
 // Arithmetic per pair: identical to K2 (stein_math.hpp), so results are bit-identical to st_greedy's
 // launch-per-step path and to the C bit model.
+#include <type_traits>
+
 #include "stein_math.hpp"
 #include "stein_internal.hpp"
 
@@ -31,6 +33,7 @@ __device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minl
 
 struct Scratch {          // small per-block scratch at the start of the dynamic LDS region
     double row[2 * kMaxCtDim + 2];
+    double vblk;          // this block's last published minimum (NaN iff some row's A is NaN)
     double v[kMaxPWaves];
     int64_t i[kMaxPWaves];
     int abort;
@@ -45,6 +48,26 @@ __device__ __forceinline__ void scan_take(double a, uint32_t ia, double& b, uint
     const bool take = (a < b) | (__builtin_isnan(a) & !__builtin_isnan(b));
     b = take ? a : b;
     ib = take ? ia : ib;
+}
+
+// The same when no A of the block can be NaN (fast variant: see greedy_persistent): plain '<'.
+template <bool NANFREE>
+__device__ __forceinline__ void scan_take_v(double a, uint32_t ia, double& b, uint32_t& ib) {
+    if constexpr (NANFREE) {
+        const bool take = a < b;
+        b = take ? a : b;
+        ib = take ? ia : ib;
+    } else {
+        scan_take(a, ia, b, ib);
+    }
+}
+
+// value known to be identical in every lane: move it to SGPRs
+__device__ __forceinline__ double uniform(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v);
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
 }  // namespace
@@ -68,7 +91,7 @@ struct PersistArgs {
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
 // every block records s_memrealtime (100 MHz, chip-wide clock) at each phase of steps
 // [kStampFirst, kStampFirst + kStampSteps).
-[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 6;
+[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 8;
 #ifdef ST_PERSIST_STAMPS
 #define ST_STAMP(a, t, ph)                                                                         \
     do {                                                                                            \
@@ -76,8 +99,15 @@ struct PersistArgs {
             (a).stamps[((int64_t)blockIdx.x * kStampSteps + ((t) - kStampFirst)) * kStampPhases + (ph)] = \
                 __builtin_amdgcn_s_memrealtime();                                                    \
     } while (0)
+// value-ordered stamp: taken only after `val` has been computed (an opaque use pins the order)
+#define ST_STAMP_AFTER(a, t, ph, val)                                                              \
+    do {                                                                                            \
+        asm volatile("" ::"v"(val));                                                                \
+        ST_STAMP(a, t, ph);                                                                         \
+    } while (0)
 #else
 #define ST_STAMP(a, t, ph) do { } while (0)
+#define ST_STAMP_AFTER(a, t, ph, val) do { } while (0)
 #endif
 
 // Exchange = self-validating granules (MI355X_MICROARCH.md R2: "the data IS the flag"): each block
@@ -97,6 +127,7 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
         li = sc->i[0];
 #pragma unroll
         for (int w = 1; w < NT / 64; ++w) take_if_better(sc->v[w], sc->i[w], v, li);
+        sc->vblk = v;   // read by every thread after wait_and_pick's barrier
         uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * 4;
         const uint64_t tag = (uint64_t)(uint32_t)(t + 1) << 32;
         const uint64_t vb = (uint64_t)__double_as_longlong(v);
@@ -107,9 +138,12 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
     }
 }
 
-// wave 0 sweeps the G records of step t until every tag is t+1 (bounded), reduces them
-// (np.argmin order); then the winner's row is read from the read-only x / g / w arrays into
-// sc->row.  Returns the winner's index, or -1 if the sweep timed out (grid-wide abort).
+// wave 0 sweeps the G records of step t until every tag is t+1 (bounded) and reduces them
+// (np.argmin order).  Lane L owns records L, L+64, ...: as soon as all of ITS records carry the tag
+// it reduces them and immediately loads the row (x, g[, w]) of its local best from the read-only
+// input arrays, so the winner's row is usually in registers by the time the slowest block has
+// published; after the wave MINLOC the winning lane writes that row to sc->row.  Returns the
+// winner's index, or -1 if the sweep timed out (grid-wide abort).
 template <int D, bool GF>
 __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
     const int G = gridDim.x;
@@ -121,29 +155,57 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         double v = INFINITY;
         int64_t gi = INT64_MAX;
+        bool mine = false;                 // this lane's records are complete and reduced
+        bool have_row = false;             // ... and the row of its local best is in rowv
+        double rowv[2 * D + (GF ? 1 : 0)];
+#pragma unroll
+        for (int k = 0; k < 2 * D + (GF ? 1 : 0); ++k) rowv[k] = 0.0;
+        auto load_row = [&](int64_t r) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                rowv[k] = a.x[(int64_t)k * a.ld + r];
+                rowv[D + k] = a.g[(int64_t)k * a.ld + r];
+            }
+            if constexpr (GF) rowv[2 * D] = a.w[r];
+        };
         int ok_all = 1;
         for (unsigned it = 0;; ++it) {
-            bool ok = true;
-            v = INFINITY;
-            gi = INT64_MAX;
+            bool fresh = false;
+            if (!mine) {
+                bool ok = true;
+                double lv = INFINITY;
+                int64_t li = INT64_MAX;
 #pragma unroll
-            for (int c = 0; c < kMaxGrid / 64; ++c) {
-                const int r = lane + 64 * c;
-                if (r < G) {
-                    const uint64_t* gr = bank + (int64_t)r * 4;
-                    const uint64_t g0 = __hip_atomic_load(gr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t g1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t g2 = __hip_atomic_load(gr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    ok &= ((uint32_t)(g0 >> 32) == want) & ((uint32_t)(g1 >> 32) == want) &
-                          ((uint32_t)(g2 >> 32) == want);
-                    const double rv = __longlong_as_double(
-                        (long long)((g1 << 32) | (g0 & 0xFFFFFFFFull)));
-                    const uint32_t ib = (uint32_t)g2;
-                    const int64_t ri = ib == 0xFFFFFFFFu ? INT64_MAX : (int64_t)ib;
-                    if (better(rv, ri, v, gi)) { v = rv; gi = ri; }
+                for (int c = 0; c < kMaxGrid / 64; ++c) {
+                    const int r = lane + 64 * c;
+                    if (r < G) {
+                        const uint64_t* gr = bank + (int64_t)r * 4;
+                        const uint64_t g0 = __hip_atomic_load(gr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t g1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        const uint64_t g2 = __hip_atomic_load(gr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                        ok &= ((uint32_t)(g0 >> 32) == want) & ((uint32_t)(g1 >> 32) == want) &
+                              ((uint32_t)(g2 >> 32) == want);
+                        const double rv = __longlong_as_double(
+                            (long long)((g1 << 32) | (g0 & 0xFFFFFFFFull)));
+                        const uint32_t ib = (uint32_t)g2;
+                        const int64_t ri = ib == 0xFFFFFFFFu ? INT64_MAX : (int64_t)ib;
+                        if (better(rv, ri, lv, li)) { lv = rv; li = ri; }
+                    }
+                }
+                if (ok) {
+                    mine = true;
+                    fresh = true;
+                    v = lv;
+                    gi = li;
                 }
             }
-            if (__all(ok)) break;
+            if (__all(mine)) break;
+            // speculative row loads only while other lanes still wait: loads issued in the final
+            // iteration would hold up the (in-order) vmcnt wait before the winner's row is used
+            if (fresh && gi != INT64_MAX) {
+                load_row(gi);
+                have_row = true;
+            }
             __builtin_amdgcn_s_sleep(1);
             if ((it & 15) == 15) {
                 const bool late = __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks;
@@ -153,7 +215,14 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             }
         }
         ST_STAMP(a, t + 1, 1);
+        const int64_t my = gi;
         p_wave_minloc(v, gi);
+        // record indices are distinct across blocks, so exactly one lane holds the winner
+        if (ok_all && my == gi && gi != INT64_MAX) {
+            if (!have_row) load_row(gi);
+#pragma unroll
+            for (int k = 0; k < 2 * D + (GF ? 1 : 0); ++k) sc->row[k] = rowv[k];
+        }
         if (lane == 0) {
             if (!ok_all) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sc->abort = !ok_all;
@@ -161,19 +230,9 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         }
     }
     __syncthreads();
-    if (sc->abort) return -1;
-    const int64_t gi = sc->i[0];
-    const int k = threadIdx.x;
-    if (k < 2 * D + (GF ? 1 : 0)) {
-        double val;
-        if (k < D) val = a.x[(int64_t)k * a.ld + gi];
-        else if (k < 2 * D) val = a.g[(int64_t)(k - D) * a.ld + gi];
-        else val = a.w[gi];
-        sc->row[k] = val;
-    }
-    __syncthreads();
     ST_STAMP(a, t + 1, 2);
-    return gi;
+    if (sc->abort) return -1;
+    return sc->i[0];
 }
 
 template <int D, bool GF, int RT, int NT>
@@ -195,8 +254,11 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
     const double l = a.l, l2 = a.l * a.l, tr = a.tr;
 
     // ---- stage the block's rows on chip ----------------------------------------------------
+    // and decide whether every row of the block admits the range-guarded fast pair arithmetic
+    // (stein_math.hpp fast_range_ok; padding rows are zeros)
     double xr[RT > 0 ? RT : 1][D], gr[RT > 0 ? RT : 1][D], ar[RT > 0 ? RT : 1];
     double wr[(GF && RT > 0) ? RT : 1];
+    int rok = fast_range_ok(l) & (int)(l > 0.0) & (int)(tr > 0.0) & (int)(tr <= 0x1p64);
 #pragma unroll
     for (int q = 0; q < RT; ++q) {
         const int64_t row = r0 + (int64_t)q * kPBlock + tid;
@@ -205,6 +267,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         for (int k = 0; k < D; ++k) {
             xr[q][k] = ok ? a.x[k * ld + row] : 0.0;
             gr[q][k] = ok ? a.g[k * ld + row] : 0.0;
+            rok &= fast_range_ok(xr[q][k]) & fast_range_ok(gr[q][k]);
         }
         if constexpr (GF) wr[q] = ok ? a.w[row] : 0.0;
     }
@@ -213,12 +276,18 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         const bool ok = row < r1;
 #pragma unroll
         for (int k = 0; k < D; ++k) {
-            sx[k * RL + e] = ok ? a.x[k * ld + row] : 0.0;
-            sg[k * RL + e] = ok ? a.g[k * ld + row] : 0.0;
+            const double xv = ok ? a.x[k * ld + row] : 0.0, gv = ok ? a.g[k * ld + row] : 0.0;
+            sx[k * RL + e] = xv;
+            sg[k * RL + e] = gv;
+            rok &= fast_range_ok(xv) & fast_range_ok(gv);
         }
         if constexpr (GF) sw[e] = ok ? a.w[row] : 0.0;
     }
-    __syncthreads();
+    for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) rok &= fast_range_ok(a.x[k * ld + row]) & fast_range_ok(a.g[k * ld + row]);
+    }
+    const int block_fast = __syncthreads_and(rok);
 
     // ---- step 0: diagonal --------------------------------------------------------------------
     // running best of this thread: starts at its first row (register row 0, which precedes all its
@@ -230,9 +299,8 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         const int64_t row = r0 + (int64_t)q * kPBlock + tid;
         double kv = diag_value_ct<D>(gr[q], tr);
         if constexpr (GF) kv = (kv * wr[q]) * wr[q];
-        ar[q] = kv;
-        const double cand = row < r1 ? kv : INFINITY;
-        if (q == 0) { bv = cand; bi = (uint32_t)row; } else scan_take(cand, (uint32_t)row, bv, bi);
+        ar[q] = row < r1 ? kv : INFINITY;   // padding rows hold +inf for the whole run
+        if (q == 0) { bv = ar[q]; bi = (uint32_t)row; } else scan_take(ar[q], (uint32_t)row, bv, bi);
     }
     for (int e = tid; e < RL; e += kPBlock) {
         const int64_t row = lds_base + e;
@@ -241,8 +309,9 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         for (int k = 0; k < D; ++k) gi[k] = sg[k * RL + e];
         double kv = diag_value_ct<D>(gi, tr);
         if constexpr (GF) kv = (kv * sw[e]) * sw[e];
+        kv = row < r1 ? kv : INFINITY;
         sa[e] = kv;
-        scan_take(row < r1 ? kv : INFINITY, (uint32_t)row, bv, bi);
+        scan_take(kv, (uint32_t)row, bv, bi);
     }
     for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
         double gi[D];
@@ -262,59 +331,122 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         if (win < 0) break;
         if (blockIdx.x == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
         double xj[D], gj[D];
+        // fast variant: range-guarded arithmetic (block rows and winner row in range) and a
+        // NaN-free scan -- valid while no A of this block is NaN: the block's last minimum is NaN
+        // iff one is, and fast steps keep finite sums finite (|2k| < 2^191 per step)
+        int wfast = (block_fast != 0) & (int)!__builtin_isnan(sc->vblk);
 #pragma unroll
-        for (int k = 0; k < D; ++k) { xj[k] = sc->row[k]; gj[k] = sc->row[D + k]; }
-        const double wj = GF ? sc->row[2 * D] : 1.0;
-        // first streamed row: issue its loads now, they land while the on-chip rows compute
-        int64_t srow = str_base + tid;
-        bool have = srow < r1;
-        double nx[D], ng[D], na = 0.0, nw = 1.0;
-        if (have) {
-#pragma unroll
-            for (int k = 0; k < D; ++k) { nx[k] = a.x[k * ld + srow]; ng[k] = a.g[k * ld + srow]; }
-            na = a.A[srow];
-            if constexpr (GF) nw = a.w[srow];
+        for (int k = 0; k < D; ++k) {
+            // block-uniform: keep the winner row in SGPRs (VALU fp64 ops take one scalar operand)
+            xj[k] = uniform(sc->row[k]);
+            gj[k] = uniform(sc->row[D + k]);
+            wfast &= fast_range_ok(xj[k]) & fast_range_ok(gj[k]);
         }
+        const double wj = GF ? uniform(sc->row[2 * D]) : 1.0;
+        // one block-uniform choice per step: range-guarded fast arithmetic or the general one
+        auto sweep_rows = [&](auto fast_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value;
+            // opaque marker: keeps LLVM from if-converting the two variants into
+            // compute-both-and-select (both are pure arithmetic over the register rows)
+            asm volatile(";; sweep_rows variant" ::);
+            // streamed rows go two at a time; the first pair's loads are issued now and land while
+            // the on-chip rows compute.  Addresses of rows past r1 are clamped to r0 (a valid row
+            // of this block): their loads are harmless and their results are dropped.
+            struct SRow { double x[D], g[D], a, w; };
+            auto fetch = [&](int64_t row, SRow& r) {
+                const int64_t rr = row < r1 ? row : r0;
 #pragma unroll
-        for (int q = 0; q < RT; ++q) {
-            const int64_t row = r0 + (int64_t)q * kPBlock + tid;
-            double kv = pair_value_ct<D>(xr[q], gr[q], xj, gj, l, l2, tr);
-            if constexpr (GF) kv = (kv * wr[q]) * wj;
-            ar[q] = ar[q] + 2.0 * kv;
-            const double cand = row < r1 ? ar[q] : INFINITY;
-            if (q == 0) { bv = cand; bi = (uint32_t)row; } else scan_take(cand, (uint32_t)row, bv, bi);
-        }
-        for (int e = tid; e < RL; e += kPBlock) {
-            const int64_t row = lds_base + e;
-            double xi[D], gi[D];
+                for (int k = 0; k < D; ++k) { r.x[k] = a.x[k * ld + rr]; r.g[k] = a.g[k * ld + rr]; }
+                r.a = a.A[rr];
+                r.w = GF ? a.w[rr] : 1.0;
+            };
+            // (with two waves per SIMD the registers are too tight to carry the prefetched pair
+            // through the on-chip rows: the 512-thread variant issues it after them)
+            constexpr bool kEarlyStream = NT <= 256;
+            int64_t srow = str_base + tid;
+            // opaque per step: otherwise LICM hoists the ~20 64-bit load addresses of the first
+            // streamed pair out of the step loop and they end up spilled to scratch
+            asm volatile("" : "+v"(srow));
+            SRow c0, c1;
+            if (kEarlyStream && srow < r1) { fetch(srow, c0); fetch(srow + kPBlock, c1); }
+            // register rows: track the slot q (a constant) and convert it to the row once
+            uint32_t bq = 0;
 #pragma unroll
-            for (int k = 0; k < D; ++k) { xi[k] = sx[k * RL + e]; gi[k] = sg[k * RL + e]; }
-            double kv = pair_value_ct<D>(xi, gi, xj, gj, l, l2, tr);
-            if constexpr (GF) kv = (kv * sw[e]) * wj;
-            const double av = sa[e] + 2.0 * kv;
-            sa[e] = av;
-            scan_take(row < r1 ? av : INFINITY, (uint32_t)row, bv, bi);
-        }
-        while (have) {   // streamed rows, one row of loads kept in flight ahead of the compute
-            double xi[D], gi[D];
-#pragma unroll
-            for (int k = 0; k < D; ++k) { xi[k] = nx[k]; gi[k] = ng[k]; }
-            const double ai = na, wi = nw;
-            const int64_t row = srow;
-            srow += kPBlock;
-            have = srow < r1;
-            if (have) {
-#pragma unroll
-                for (int k = 0; k < D; ++k) { nx[k] = a.x[k * ld + srow]; ng[k] = a.g[k * ld + srow]; }
-                na = a.A[srow];
-                if constexpr (GF) nw = a.w[srow];
+            for (int q = 0; q < RT; ++q) {
+                const int64_t row = r0 + (int64_t)q * kPBlock + tid;
+                double kv = pair_value_ct<D, FAST>(xr[q], gr[q], xj, gj, l, l2, tr);
+                if constexpr (GF) kv = (kv * wr[q]) * wj;
+                // padding rows (zeros) keep A = +inf: in the fast range k is finite, so
+                // inf + 2k = inf needs no mask; the general path masks the update instead
+                if constexpr (FAST) ar[q] = add_twice<true>(ar[q], kv);
+                else ar[q] = row < r1 ? add_twice<false>(ar[q], kv) : INFINITY;
+                (void)row;
+                if (q == 0) { bv = ar[q]; bq = 0; } else scan_take_v<FAST>(ar[q], (uint32_t)q, bv, bq);
+                // two waves per SIMD hide latency by themselves: cap the scheduler's interleaving
+                // of independent rows (it costs registers the 512-thread variant does not have)
+                if constexpr (NT >= 512) {
+                    if ((q & 1) == 1) __builtin_amdgcn_sched_barrier(0);
+                }
             }
-            double kv = pair_value_ct<D>(xi, gi, xj, gj, l, l2, tr);
-            if constexpr (GF) kv = (kv * wi) * wj;
-            const double av = ai + 2.0 * kv;
-            a.A[row] = av;
-            scan_take(av, (uint32_t)row, bv, bi);
-        }
+            bi = (uint32_t)(r0 + tid) + bq * (uint32_t)kPBlock;
+            ST_STAMP_AFTER(a, t, 5, bv);
+            // LDS rows, UL per iteration: independent dependency chains for the scheduler
+            // (one wave per SIMD: a single chain leaves the fp64 pipe idle between dependent ops).
+            // RL is a multiple of 64, so the trip counts are wave-uniform.
+            auto lds_pair = [&](int e) -> double {
+                const int64_t row = lds_base + e;
+                double xi[D], gi[D];
+#pragma unroll
+                for (int k = 0; k < D; ++k) { xi[k] = sx[k * RL + e]; gi[k] = sg[k * RL + e]; }
+                double kv = pair_value_ct<D, FAST>(xi, gi, xj, gj, l, l2, tr);
+                if constexpr (GF) kv = (kv * sw[e]) * wj;
+                double av;
+                if constexpr (FAST) av = add_twice<true>(sa[e], kv);
+                else av = row < r1 ? add_twice<false>(sa[e], kv) : INFINITY;
+                sa[e] = av;
+                return av;
+            };
+            // (two waves per SIMD: two chains per wave are enough and leave room for the rows)
+            constexpr int UL = NT >= 512 ? 2 : 4;
+            int e = tid;
+            for (; e + (UL - 1) * kPBlock < RL; e += UL * kPBlock) {
+                double av[UL];
+#pragma unroll
+                for (int u = 0; u < UL; ++u) av[u] = lds_pair(e + u * kPBlock);
+#pragma unroll
+                for (int u = 0; u < UL; ++u)
+                    scan_take_v<FAST>(av[u], (uint32_t)(lds_base + e + u * kPBlock), bv, bi);
+            }
+            for (; e < RL; e += kPBlock) scan_take_v<FAST>(lds_pair(e), (uint32_t)(lds_base + e), bv, bi);
+            ST_STAMP_AFTER(a, t, 6, bv);
+            // streamed rows: two per iteration, the next two rows' loads in flight meanwhile
+            auto stream_pair = [&](const SRow& r) -> double {
+                double kv = pair_value_ct<D, FAST>(r.x, r.g, xj, gj, l, l2, tr);
+                if constexpr (GF) kv = (kv * r.w) * wj;
+                return add_twice<FAST>(r.a, kv);
+            };
+            if (!kEarlyStream && srow < r1) { fetch(srow, c0); fetch(srow + kPBlock, c1); }
+            while (srow < r1) {
+                const int64_t nrow = srow + 2 * kPBlock;
+                SRow n0, n1;
+                fetch(nrow, n0);
+                fetch(nrow + kPBlock, n1);
+                const double av0 = stream_pair(c0);
+                const double av1 = stream_pair(c1);
+                const bool ok1 = srow + kPBlock < r1;
+                a.A[srow] = av0;
+                if (ok1) a.A[srow + kPBlock] = av1;
+                scan_take_v<FAST>(av0, (uint32_t)srow, bv, bi);
+                scan_take_v<FAST>(ok1 ? av1 : INFINITY, (uint32_t)(srow + kPBlock), bv, bi);
+                c0 = n0;
+                c1 = n1;
+                srow = nrow;
+            }
+        };
+        // the flag is block-uniform (same LDS row, same block flag): make that explicit so the
+        // branch is scalar and the two variants stay separate code paths
+        if (__builtin_amdgcn_readfirstlane(wfast)) sweep_rows(std::true_type{});
+        else sweep_rows(std::false_type{});
         ST_STAMP(a, t, 3);
         publish<NT>(a, sc, bv, bi, t);
         ST_STAMP(a, t, 4);
@@ -388,6 +520,7 @@ template <int D, bool GF>
 static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int G, size_t lds, hipStream_t s) {
     if (nt == 512) {
         if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s);
+        if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s);
         return launch_p<D, GF, 8, 512>(a, G, lds, s);
     }
     switch (rt) {
@@ -403,7 +536,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
                                     int* used) {
     *used = 0;
-    if (g_persist_rt == 0 || (d != 2 && d != 4) || m < 1 || m >= 0xFFFFFFFFll || n >= 0xFFFFFFFFll)
+    // 32-bit row indices, padding rows included (< n + one block's register rows)
+    if (g_persist_rt == 0 || (d != 2 && d != 4) || m < 1 || m >= 0xFFFFFFFFll || n >= 0x7FFFFFFFll)
         return hipErrorNotSupported;
     int dev = 0, cus = 0, lds_max = 0, lds_optin = 0, coop = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
@@ -426,9 +560,10 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     const int nt = g_persist_nt > 0 ? g_persist_nt : 256;
     const int rt_max = nt == 512 ? 8 : 16;
     int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
-    if (rt != 4 && rt != 8 && rt != 16) rt = rt_max;
+    if (rt != 4 && rt != 6 && rt != 8 && rt != 16) rt = rt_max;
     if (rt > rt_max) rt = rt_max;
-    while (rt > 4 && (int64_t)rt * nt > R) rt /= 2;   // do not hold empty register rows
+    if (rt == 6 && nt != 512) rt = 8;
+    while (rt > 4 && (int64_t)rt * nt > R) rt = rt == 6 ? 4 : rt / 2;   // no empty register rows
     const bool gf = w != nullptr;
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);
     const size_t head = (sizeof(Scratch) + 15) / 16 * 16;

@@ -48,11 +48,88 @@ __device__ __forceinline__ double finish_pair(double qs, double t1s, double t2s,
     return (t1 + t2) + t3;
 }
 
+// ---- range-guarded fast path ---------------------------------------------------------------
+// When every coordinate and score component of BOTH points is 0 or has magnitude in
+// [2^-60, 2^60], and l is in [2^-60, 2^60] (fast_range_ok), every intermediate of the pair is 0 or
+// a normal number far from the limits: differences are 0 or >= 2^-112 (multiples of 2^-112),
+// per-k products 0 or in [2^-344, 2^242], their sums 0 or >= 2^-396 (multiples of the smallest
+// ulp), qf in [1, 2^185], p25 <= 2^463, and every quotient is normal.  In that range
+//   * the compiler's IEEE f64 division sequence (v_div_scale x2, v_rcp, 2 Newton steps, v_mul,
+//     residual fma, v_div_fmas, v_div_fixup) never scales: div_scale returns its operand with
+//     VCC = 0, div_fmas is a plain fma and div_fixup returns the quotient unchanged;
+//   * its sqrt sequence (scale-if-below-2^-767, v_rsq, Goldschmidt + 2 residual corrections,
+//     +0/-0/+inf class fix-up) never scales and never takes the fix-up;
+// (|k| < 2^190 there, so the running-sum update A + 2k may also be the single fma(2, k, A): 2k is
+// exact.)  So fast_div / fast_sqrt below -- the same sequences without those steps -- return the same bits
+// as '/' and sqrt, correctly rounded.  The only deviations are signs of zero: a -0 numerator gives
+// +0 instead of -0 in t1/t3, and t3s drops the leading "0.0 +".  k = fl(fl(t1 + t2) + t3) is
+// unaffected because t2 = fl(tr + t2s) / p15 is never -0 (tr > 0), so a zero t1 or t3 only ever
+// meets a t2 (or t1 + t2) that is +0 or non-zero.
+// A + 2k: fl(A + fl(2k)); in the fast range 2k is exact, so one fma gives the same bits
+template <bool FAST>
+__device__ __forceinline__ double add_twice(double A, double k) {
+    if constexpr (FAST) return __builtin_fma(2.0, k, A);
+    else return A + 2.0 * k;
+}
+
+__device__ __forceinline__ int fast_range_ok(double v) {   // 1 / 0, branch-free
+    const double a = __builtin_fabs(v);
+    return (int)(a == 0.0) | ((int)(a >= 0x1p-60) & (int)(a <= 0x1p60));
+}
+
+__device__ __forceinline__ double fast_sqrt(double x) {   // x in [1, 2^185]
+    double g = x * __builtin_amdgcn_rsq(x);
+    double h = __builtin_amdgcn_rsq(x) * 0.5;
+    const double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double dd = __builtin_fma(-g, g, x);
+    g = __builtin_fma(dd, h, g);
+    dd = __builtin_fma(-g, g, x);
+    return __builtin_fma(dd, h, g);
+}
+
+__device__ __forceinline__ double fast_div(double a, double b) {   // b in [1, 2^463], a/b normal or 0
+    double r = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    e = __builtin_fma(-b, r, 1.0);
+    r = __builtin_fma(r, e, r);
+    const double q = a * r;
+    const double rem = __builtin_fma(-b, q, a);
+    return __builtin_fma(rem, r, q);
+}
+
+__device__ __forceinline__ double finish_pair_fast(double qs, double t1s, double t2s, double t3s,
+                                                   double tr) {
+    const double q = 1.0 + qs;
+    const double s = fast_sqrt(q);
+    const double e = __builtin_fma(-s, s, q);
+    // e is a multiple of 2^-104 (s >= 1), so 0.5*e is exact and (0.5*s)*e == s*(0.5*e) exactly
+    const double he = 0.5 * e;
+    const double hi = q * s;
+    double lo = __builtin_fma(q, s, -hi);
+    lo = __builtin_fma(s, he, lo);
+    const double p15 = hi + lo;
+    const double q2 = q * q;
+    const double q2lo = __builtin_fma(q, q, -q2);
+    const double hi2 = q2 * s;
+    double lo2 = __builtin_fma(q2, s, -hi2);
+    lo2 = __builtin_fma(q2lo, s, lo2);
+    lo2 = __builtin_fma(hi, he, lo2);
+    const double p25 = hi2 + lo2;
+    const double t1 = fast_div(-3.0 * t1s, p25);
+    const double t2 = fast_div(tr + t2s, p15);
+    const double t3 = fast_div(t3s, s);
+    return (t1 + t2) + t3;
+}
+
 // t3 follows NumPy pairwise_sum streamed over k (no product array): 0 + e0 + ... for d < 8;
 // 8 partial sums for 8 <= d <= 128.  (d > 128 rejected at the ABI.)
 
 // Compile-time d (D >= 1): everything unrolled, vectors in registers.
-template <int D>
+// FAST: caller guarantees fast_range_ok for both points' components and for l (see above).
+template <int D, bool FAST = false>
 __device__ __forceinline__ double pair_value_ct(const double (&xi)[D], const double (&gi)[D],
                                                 const double* xj, const double* gj, double l,
                                                 double l2, double tr) {
@@ -71,7 +148,11 @@ __device__ __forceinline__ double pair_value_ct(const double (&xi)[D], const dou
         }
     }
     double t3s;
-    if constexpr (D < 8) {
+    if constexpr (D < 8 && FAST) {
+        t3s = gi[0] * gj[0];   // "0.0 +" dropped: differs only in the sign of a zero t3s
+#pragma unroll
+        for (int k = 1; k < D; ++k) t3s += gi[k] * gj[k];
+    } else if constexpr (D < 8) {
         t3s = 0.0;
 #pragma unroll
         for (int k = 0; k < D; ++k) t3s += gi[k] * gj[k];
@@ -87,7 +168,8 @@ __device__ __forceinline__ double pair_value_ct(const double (&xi)[D], const dou
 #pragma unroll
         for (int k = full; k < D; ++k) t3s += gi[k] * gj[k];
     }
-    return finish_pair(qs, t1s, t2s, t3s, tr);
+    if constexpr (FAST) return finish_pair_fast(qs, t1s, t2s, t3s, tr);
+    else return finish_pair(qs, t1s, t2s, t3s, tr);
 }
 
 // Diagonal k(x, x) = fl(tr + PAIRWISE fl(g_k*g_k)) (dk = 0: qf = 1, t1 = -0, pow(1, .) = 1).

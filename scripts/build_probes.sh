@@ -1,0 +1,15 @@
+#!/usr/bin/env bash
+# Build the measurement probes (not product code): tools/probe against the product library, and
+# tools/_diag/probe_stamps against a diagnostic copy of the library built with -DST_PERSIST_STAMPS.
+set -eu
+cd "$(dirname "$0")/.."
+LIB=gradient-free-mcmc-postprocessing_amd/stein_thinning/_lib
+CS=gradient-free-mcmc-postprocessing_amd/csrc
+HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+$HIPCC --offload-arch=gfx950 -O3 -std=c++17 -o tools/probe tools/probe.hip -L$LIB -lstein_hip -Wl,-rpath,'$ORIGIN/../'$LIB
+mkdir -p tools/_diag
+$HIPCC --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -DST_PERSIST_STAMPS \
+  -o tools/_diag/libstein_hip.so $CS/capi.hip $CS/greedy.hip $CS/persistent.hip $CS/pairwise.hip
+$HIPCC --offload-arch=gfx950 -O3 -std=c++17 -DST_PERSIST_STAMPS -o tools/_diag/probe_stamps tools/probe.hip \
+  -Ltools/_diag -lstein_hip -Wl,-rpath,'$ORIGIN'
+echo built

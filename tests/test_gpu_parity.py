@@ -174,6 +174,37 @@ def test_persistent_and_fallback_bit_exact(tune):
     assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
 
 
+@pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
+def test_persistent_exact_path_outside_fast_range(d, gf):
+    """Rows with components outside [2^-60, 2^60] (tiny / huge scores, tiny coordinates) force the
+    persistent kernel's general arithmetic for their blocks and for steps whose selected row is
+    out of range (csrc/stein_math.hpp fast_range_ok); results stay bit-identical to the C model."""
+    n, m = 200_003, 40
+    x, g = _rw_chain(n, d, seed=7 + d)
+    s, gs = o._validate_and_standardize(x, g, True)
+    rng = np.random.default_rng(d)
+    rows = rng.choice(n, size=12, replace=False)
+    gs = gs.copy()
+    s = s.copy()
+    gs[rows[:4], 0] = 1e-25          # tiny score component: small diagonal -> selected early
+    gs[rows[4:6], :] = 3e-22
+    gs[rows[6:8], -1] = 2e19         # huge component
+    s[rows[8:10], 0] = 1e-30         # tiny coordinate
+    gs[rows[10:], :] = 0.0           # exact zeros are inside the fast range
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    w = None
+    if gf:
+        lw = -0.2 * np.sum(x * x, axis=1)
+        w = np.exp(lw - lw.min())
+    idx, A = DeviceProblem(s, gs, w, l, tr).greedy(m, return_sums=True)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    np.testing.assert_array_equal(idx, cidx)
+    assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
+    if not gf:   # Langevin: the tiny-score rows have the smallest diagonal and are selected
+        assert np.intersect1d(idx, rows[:6]).size > 0
+
+
 @pytest.mark.parametrize('d', [2, 4, 9, 50])
 def test_pair_values_bit_exact_vs_c_model(d):
     x, g = _rw_chain(700, d, seed=100 + d)

@@ -162,7 +162,7 @@ int main(int argc, char** argv) {
     st_tune(0, 256); st_tune(1, -1); st_tune(2, -1);
     // whole-run st_greedy: persistent kernel (register rows per thread rt; 0 = launch per step)
     struct V { int rt, nt; };
-    for (V cfg : {V{8, 512}, V{4, 512}, V{16, 256}, V{8, 256}, V{0, 256}}) {
+    for (V cfg : {V{8, 512}, V{6, 512}, V{4, 512}, V{16, 256}, V{0, 256}}) {
         const int rt = cfg.rt;
         st_tune(3, rt);
         st_tune(4, cfg.nt);
@@ -183,7 +183,7 @@ int main(int argc, char** argv) {
     st_tune(4, -1);
 #ifdef ST_PERSIST_STAMPS
     {   // phase breakdown of persistent steps 20..51 (s_memrealtime, 10 ns ticks)
-        const int SP = 32, PH = 6, GMAX = 256;
+        const int SP = 32, PH = 8, GMAX = 256;
         uint64_t* dst;
         CK(hipMalloc(&dst, sizeof(uint64_t) * GMAX * SP * PH));
         CK(hipMemset(dst, 0, sizeof(uint64_t) * GMAX * SP * PH));
@@ -195,15 +195,17 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(h.data(), dst, h.size() * 8, hipMemcpyDeviceToHost));
         int G = 0;
         while (G < GMAX && h[(size_t)G * SP * PH + 0] != 0) ++G;
-        double acc[8] = {0};
+        double acc[8] = {0}, ph_lds = 0;
         int cnt = 0;
         for (int st = 1; st + 1 < SP; ++st) {   // step st: compute (2->3), publish (3->4), exchange
             uint64_t last_pub = 0, first_start = ~(uint64_t)0, last_start = 0;
-            double c_avg = 0, wait_avg = 0, row_avg = 0, pub_avg = 0;
+            double c_avg = 0, wait_avg = 0, row_avg = 0, pub_avg = 0, creg = 0, clds = 0;
             for (int b = 0; b < G; ++b) {
                 const uint64_t* q = &h[((size_t)b * SP + st) * PH];
                 last_pub = std::max<uint64_t>(last_pub, q[4]);
                 c_avg += (double)(q[3] - q[2]);
+                creg += (double)(q[5] - q[2]);
+                clds += (double)(q[6] - q[5]);
                 pub_avg += (double)(q[4] - q[3]);
                 const uint64_t* nx = &h[((size_t)b * SP + st + 1) * PH];
                 wait_avg += (double)(nx[1] - nx[0]);
@@ -219,12 +221,16 @@ int main(int argc, char** argv) {
                 s1 = std::min<uint64_t>(s1, h[((size_t)b * SP + st + 1) * PH + 2]);
             }
             acc[6] += (double)(s1 - s0);
+            acc[7] += creg / G;
+            ph_lds += clds / G;
             ++cnt;
         }
         printf("stamps G=%d (us): compute %.2f  publish %.2f  sweep-wait %.2f  winner-row %.2f  "
                "last-publish->first-next-start %.2f  start-skew %.2f  step period %.2f\n", G,
                acc[0] / cnt / 100, acc[1] / cnt / 100, acc[2] / cnt / 100, acc[3] / cnt / 100,
                acc[4] / cnt / 100, acc[5] / cnt / 100, acc[6] / cnt / 100);
+        printf("compute split (us): register rows %.2f  LDS rows %.2f  streamed rows %.2f\n",
+               acc[7] / cnt / 100, ph_lds / cnt / 100, (acc[0] - acc[7] - ph_lds) / cnt / 100);
     }
 #endif
     T.start(s);
