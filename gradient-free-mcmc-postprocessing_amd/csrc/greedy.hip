@@ -24,7 +24,7 @@ namespace st {
 constexpr int kBlock = 256;
 constexpr int kWaves = kBlock / 64;
 
-__device__ __forceinline__ void wave_minloc(double& v, int64_t& i) { wave_minloc_dpp(v, i); }
+// wave_minloc (stein_math.hpp): needs every lane of the wave active -- true at each call site.
 
 // Block-wide MINLOC; result valid in every thread.
 __device__ __forceinline__ void block_minloc(double& v, int64_t& i, double* s_v, int64_t* s_i) {

@@ -6,15 +6,16 @@
 //   * Its rows live on chip for the whole run: RT rows per thread in VGPRs/AGPRs (x, g, A[, w]),
 //     RL rows in LDS (SoA), the remainder streamed from HBM each step (coalesced, like K2).
 //   * Per step: every block evaluates k(x_i, x_j) for its rows, A_i += 2k, block MINLOC, and
-//     publishes ONE record {A_min, index} as three data-tagged 8-byte granules (tag = step + 1;
+//     publishes ONE record {A_min, index} as two data-tagged 8-byte granules (8-bit step tag;
 //     MI355X_MICROARCH.md recipe R2, "the data IS the flag": no fence, no counter).  One wave per
 //     block sweeps all G records until every tag matches, reduces them (np.argmin order) and the
 //     block reads the winner's row from the read-only x / g / w arrays -> next step.  Block 0
 //     writes idx.  Two record banks alternate by step parity.
 //   * Every spin is bounded by a wall-clock timeout (s_memrealtime); a timeout sets status[0] and
 //     every block leaves the step loop, so the grid always drains.
-// Arithmetic per pair: identical to K2 (stein_math.hpp), so results are bit-identical to st_greedy's
-// launch-per-step path and to the C bit model.
+// Arithmetic per pair: K2's (stein_math.hpp) or, when the block's rows and the winner lie in the
+// guarded range, its division/sqrt-light form that returns the same bits (fast_div / fast_sqrt):
+// results are bit-identical to st_greedy's launch-per-step path and to the C bit model.
 #include <type_traits>
 
 #include "stein_math.hpp"
@@ -29,7 +30,7 @@ constexpr int kShards = 8;
 constexpr int kMaxGrid = 256;               // one block per CU on MI355X (256 CUs)
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
 
-__device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minloc_dpp(v, i); }
+__device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minloc(v, i); }
 
 struct Scratch {          // small per-block scratch at the start of the dynamic LDS region
     double row[2 * kMaxCtDim + 2];
@@ -81,7 +82,7 @@ struct PersistArgs {
     double l, tr;
     int64_t m;            // n_points
     uint32_t* idx_out;
-    uint64_t* gran;       // 2 banks x G records x 4 granules (3 used)
+    uint64_t* gran;       // 2 banks x G records x 2 granules
     unsigned* status;     // [0]: 0 ok, 1 timeout
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
@@ -91,7 +92,7 @@ struct PersistArgs {
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
 // every block records s_memrealtime (100 MHz, chip-wide clock) at each phase of steps
 // [kStampFirst, kStampFirst + kStampSteps).
-[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 8;
+[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 10;
 #ifdef ST_PERSIST_STAMPS
 #define ST_STAMP(a, t, ph)                                                                         \
     do {                                                                                            \
@@ -111,9 +112,15 @@ struct PersistArgs {
 #endif
 
 // Exchange = self-validating granules (MI355X_MICROARCH.md R2: "the data IS the flag"): each block
-// publishes {A_min, index} for step t as three 8-byte granules {tag = t+1 : 32-bit payload}
-// (value low word, value high word, index), each written by ONE aligned 8-B agent-scope store.
-// A consumer accepts a record only when all three tags equal t+1; banks alternate by step parity.
+// publishes {A_min, index} for step t as ONE 16-byte record of two 8-byte granules, each written
+// by one aligned 8-B agent-scope store and each carrying the 8-bit tag (t+1) mod 256 in its top
+// byte:   g0 = tag:8 | value bits 63..8         g1 = tag:8 | pad:16 | value bits 7..0 | index:32
+// A consumer accepts a record only when both tags match.  Banks alternate by step parity, so a
+// slot's stale content is exactly two steps old (tag t-1): an 8-bit tag cannot alias it.
+constexpr int kRecGranules = 2;
+
+__device__ __forceinline__ uint64_t step_tag(int64_t t) { return (uint64_t)((t + 1) & 0xFF) << 56; }
+
 template <int NT>
 __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, uint32_t row,
                                         int64_t t) {
@@ -122,44 +129,50 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) { sc->v[wave] = v; sc->i[wave] = li; }
     __syncthreads();
-    if (threadIdx.x == 0) {   // ONE lane combines the wave minima and stores the three granules
+    if (threadIdx.x == 0) {   // ONE lane combines the wave minima and stores the two granules
         v = sc->v[0];
         li = sc->i[0];
 #pragma unroll
         for (int w = 1; w < NT / 64; ++w) take_if_better(sc->v[w], sc->i[w], v, li);
         sc->vblk = v;   // read by every thread after wait_and_pick's barrier
-        uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * 4;
-        const uint64_t tag = (uint64_t)(uint32_t)(t + 1) << 32;
+        uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * kRecGranules;
+        const uint64_t tag = step_tag(t);
         const uint64_t vb = (uint64_t)__double_as_longlong(v);
         const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
-        __hip_atomic_store(gr + 0, tag | (vb & 0xFFFFFFFFull), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gr + 1, tag | (vb >> 32), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gr + 2, tag | ib, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gr + 0, tag | (vb >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(gr + 1, tag | ((vb & 0xFFull) << 32) | ib, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
     }
 }
 
-// wave 0 sweeps the G records of step t until every tag is t+1 (bounded) and reduces them
-// (np.argmin order).  Lane L owns records L, L+64, ...: as soon as all of ITS records carry the tag
-// it reduces them and immediately loads the row (x, g[, w]) of its local best from the read-only
-// input arrays, so the winner's row is usually in registers by the time the slowest block has
-// published; after the wave MINLOC the winning lane writes that row to sc->row.  Returns the
-// winner's index, or -1 if the sweep timed out (grid-wide abort).
+// wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
+// (np.argmin order).  Lane L owns records L, L+64, L+128, L+192 and re-polls only those it has not
+// seen yet.  Whenever its best-so-far changes it loads that candidate's row (x, g[, w]) from the
+// read-only inputs, so the winner's row is normally in registers when the slowest block has
+// published -- except in the iteration that completes the sweep: loads issued there would hold up
+// the in-order vmcnt wait in front of the row's use.  After the wave MINLOC the winning lane
+// writes the row to sc->row.  Returns the winner's index, or -1 if the sweep timed out (grid-wide
+// abort).
 template <int D, bool GF>
 __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
+    constexpr int kRow = 2 * D + (GF ? 1 : 0);
     const int G = gridDim.x;
     ST_STAMP(a, t + 1, 0);
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const uint64_t* bank = a.gran + (t & 1) * (int64_t)G * 4;
-        const uint32_t want = (uint32_t)(t + 1);
+        const uint64_t* bank = a.gran + (t & 1) * (int64_t)G * kRecGranules;
+        const uint64_t want = step_tag(t);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        uint32_t need = 0;
+#pragma unroll
+        for (int c = 0; c < kMaxGrid / 64; ++c) need |= (lane + 64 * c < G) ? (1u << c) : 0u;
+        uint32_t seen = 0;
         double v = INFINITY;
         int64_t gi = INT64_MAX;
-        bool mine = false;                 // this lane's records are complete and reduced
-        bool have_row = false;             // ... and the row of its local best is in rowv
-        double rowv[2 * D + (GF ? 1 : 0)];
+        int64_t row_of = INT64_MAX;        // index whose row is in rowv
+        double rowv[kRow];
 #pragma unroll
-        for (int k = 0; k < 2 * D + (GF ? 1 : 0); ++k) rowv[k] = 0.0;
+        for (int k = 0; k < kRow; ++k) rowv[k] = 0.0;
         auto load_row = [&](int64_t r) {
 #pragma unroll
             for (int k = 0; k < D; ++k) {
@@ -170,41 +183,26 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         };
         int ok_all = 1;
         for (unsigned it = 0;; ++it) {
-            bool fresh = false;
-            if (!mine) {
-                bool ok = true;
-                double lv = INFINITY;
-                int64_t li = INT64_MAX;
 #pragma unroll
-                for (int c = 0; c < kMaxGrid / 64; ++c) {
-                    const int r = lane + 64 * c;
-                    if (r < G) {
-                        const uint64_t* gr = bank + (int64_t)r * 4;
-                        const uint64_t g0 = __hip_atomic_load(gr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint64_t g1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        const uint64_t g2 = __hip_atomic_load(gr + 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                        ok &= ((uint32_t)(g0 >> 32) == want) & ((uint32_t)(g1 >> 32) == want) &
-                              ((uint32_t)(g2 >> 32) == want);
+            for (int c = 0; c < kMaxGrid / 64; ++c) {
+                if ((need & ~seen) & (1u << c)) {
+                    const uint64_t* gr = bank + (int64_t)(lane + 64 * c) * kRecGranules;
+                    const uint64_t g0 = __hip_atomic_load(gr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const uint64_t g1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    if (((g0 & 0xFF00000000000000ull) == want) & ((g1 & 0xFF00000000000000ull) == want)) {
+                        seen |= 1u << c;
                         const double rv = __longlong_as_double(
-                            (long long)((g1 << 32) | (g0 & 0xFFFFFFFFull)));
-                        const uint32_t ib = (uint32_t)g2;
+                            (long long)(((g0 & 0x00FFFFFFFFFFFFFFull) << 8) | ((g1 >> 32) & 0xFFull)));
+                        const uint32_t ib = (uint32_t)g1;
                         const int64_t ri = ib == 0xFFFFFFFFu ? INT64_MAX : (int64_t)ib;
-                        if (better(rv, ri, lv, li)) { lv = rv; li = ri; }
+                        if (better(rv, ri, v, gi)) { v = rv; gi = ri; }
                     }
                 }
-                if (ok) {
-                    mine = true;
-                    fresh = true;
-                    v = lv;
-                    gi = li;
-                }
             }
-            if (__all(mine)) break;
-            // speculative row loads only while other lanes still wait: loads issued in the final
-            // iteration would hold up the (in-order) vmcnt wait before the winner's row is used
-            if (fresh && gi != INT64_MAX) {
+            if (__all(seen == need)) break;
+            if (gi != row_of && gi != INT64_MAX) {   // speculative row of the best so far
                 load_row(gi);
-                have_row = true;
+                row_of = gi;
             }
             __builtin_amdgcn_s_sleep(1);
             if ((it & 15) == 15) {
@@ -217,11 +215,17 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         ST_STAMP(a, t + 1, 1);
         const int64_t my = gi;
         p_wave_minloc(v, gi);
+        ST_STAMP(a, t + 1, 7);
         // record indices are distinct across blocks, so exactly one lane holds the winner
         if (ok_all && my == gi && gi != INT64_MAX) {
-            if (!have_row) load_row(gi);
+#ifdef ST_PERSIST_STAMPS
+            if (a.stamps && t + 1 >= kStampFirst && t + 1 < kStampFirst + kStampSteps)
+                a.stamps[((int64_t)blockIdx.x * kStampSteps + (t + 1 - kStampFirst)) * kStampPhases + 8] =
+                    row_of != gi ? 2 : 1;
+#endif
+            if (row_of != gi) load_row(gi);
 #pragma unroll
-            for (int k = 0; k < 2 * D + (GF ? 1 : 0); ++k) sc->row[k] = rowv[k];
+            for (int k = 0; k < kRow; ++k) sc->row[k] = rowv[k];
         }
         if (lane == 0) {
             if (!ok_all) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -479,9 +483,9 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
 // host side
 // ------------------------------------------------------------------------------------------
 int64_t persistent_ws_bytes(int d, int G) {
-    // [control: status (and reserved) words][2 banks x G records x 4 granules of 8 B]
+    // [control: status (and reserved) words][2 banks x G records x 2 granules of 8 B]
     (void)d;
-    return kWsControlBytes + 2 * (int64_t)G * 4 * 8;
+    return kWsControlBytes + 2 * (int64_t)G * kRecGranules * 8;
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off

@@ -317,4 +317,59 @@ __device__ __forceinline__ void wave_minloc_dpp(double& v, int64_t& i) {
     i = bi;
 }
 
+// Wave MINLOC in np.argmin order, common case first: when no lane holds a NaN (one ballot), a
+// plain v_min_f64 butterfly (DPP inside 16-lane rows, readlane across rows) gives the minimum m,
+// a ballot of v == m finds the lanes holding it, and a single such lane gives the index directly;
+// ties (several lanes equal to m, -0 == +0 included) and NaNs take the full compare chain.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v) {
+    const uint64_t vb = (uint64_t)__double_as_longlong(v);
+    const uint32_t v0 = __builtin_amdgcn_update_dpp(0u, (uint32_t)vb, CTRL, 0xF, 0xF, false);
+    const uint32_t v1 = __builtin_amdgcn_update_dpp(0u, (uint32_t)(vb >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((uint64_t)v1 << 32) | v0));
+}
+
+__device__ __forceinline__ uint64_t readlane_u64(uint64_t x, int lane) {
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)x, lane);
+    const uint32_t hi = __builtin_amdgcn_readlane((uint32_t)(x >> 32), lane);
+    return ((uint64_t)hi << 32) | lo;
+}
+
+__device__ __forceinline__ void wave_minloc(double& v, int64_t& i) {
+    if (__builtin_amdgcn_ballot_w64(__builtin_isnan(v)) != 0) {   // rare: NaN-aware chain
+        wave_minloc_dpp(v, i);
+        return;
+    }
+    double m = v;
+    m = __builtin_fmin(m, dpp_f64<0xB1>(m));    // quad_perm [1,0,3,2]
+    m = __builtin_fmin(m, dpp_f64<0x4E>(m));    // quad_perm [2,3,0,1]
+    m = __builtin_fmin(m, dpp_f64<0x124>(m));   // row_ror:4
+    m = __builtin_fmin(m, dpp_f64<0x128>(m));   // row_ror:8
+    const uint64_t mb = (uint64_t)__double_as_longlong(m);
+    const double r0 = __longlong_as_double((long long)readlane_u64(mb, 0));
+    const double r1 = __longlong_as_double((long long)readlane_u64(mb, 16));
+    const double r2 = __longlong_as_double((long long)readlane_u64(mb, 32));
+    const double r3 = __longlong_as_double((long long)readlane_u64(mb, 48));
+    m = __builtin_fmin(__builtin_fmin(r0, r1), __builtin_fmin(r2, r3));
+    const uint64_t tied = __builtin_amdgcn_ballot_w64(v == m);
+    if (__builtin_popcountll(tied) == 1) {
+        i = (int64_t)readlane_u64((uint64_t)i, __builtin_ctzll(tied));
+        v = m;
+        return;
+    }
+    // ties (duplicate MCMC rows have bit-identical sums): lowest index among the tied lanes, as
+    // a u32 min (indices < 2^32 - 1; the INT64_MAX "no row" sentinel maps to 0xFFFFFFFF)
+    uint32_t u = v == m ? (i == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)i) : 0xFFFFFFFFu;
+    u = __builtin_elementwise_min(u, (uint32_t)__builtin_amdgcn_update_dpp(0u, u, 0xB1, 0xF, 0xF, false));
+    u = __builtin_elementwise_min(u, (uint32_t)__builtin_amdgcn_update_dpp(0u, u, 0x4E, 0xF, 0xF, false));
+    u = __builtin_elementwise_min(u, (uint32_t)__builtin_amdgcn_update_dpp(0u, u, 0x124, 0xF, 0xF, false));
+    u = __builtin_elementwise_min(u, (uint32_t)__builtin_amdgcn_update_dpp(0u, u, 0x128, 0xF, 0xF, false));
+    const uint32_t u0 = __builtin_amdgcn_readlane(u, 0), u1 = __builtin_amdgcn_readlane(u, 16);
+    const uint32_t u2 = __builtin_amdgcn_readlane(u, 32), u3 = __builtin_amdgcn_readlane(u, 48);
+    const uint32_t um = __builtin_elementwise_min(__builtin_elementwise_min(u0, u1),
+                                                  __builtin_elementwise_min(u2, u3));
+    v = m;
+    i = um == 0xFFFFFFFFu ? INT64_MAX : (int64_t)um;
+}
+
 }  // namespace st

@@ -127,7 +127,10 @@ class GraphedShardedGreedy:
         torch.cuda.synchronize()
         eager_idx = self.backend.indices()
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g):
+        # thread_local: the process group's watchdog thread keeps querying events of earlier
+        # collectives while this thread captures; global mode would turn those queries into
+        # hipErrorStreamCaptureUnsupported
+        with torch.cuda.graph(g, capture_error_mode='thread_local'):
             _sharded_loop(self.backend, self.n_points, self.group)
         self.graph = g
         g.replay()

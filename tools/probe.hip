@@ -183,7 +183,7 @@ int main(int argc, char** argv) {
     st_tune(4, -1);
 #ifdef ST_PERSIST_STAMPS
     {   // phase breakdown of persistent steps 20..51 (s_memrealtime, 10 ns ticks)
-        const int SP = 32, PH = 8, GMAX = 256;
+        const int SP = 32, PH = 10, GMAX = 256;
         uint64_t* dst;
         CK(hipMalloc(&dst, sizeof(uint64_t) * GMAX * SP * PH));
         CK(hipMemset(dst, 0, sizeof(uint64_t) * GMAX * SP * PH));
@@ -229,6 +229,17 @@ int main(int argc, char** argv) {
                "last-publish->first-next-start %.2f  start-skew %.2f  step period %.2f\n", G,
                acc[0] / cnt / 100, acc[1] / cnt / 100, acc[2] / cnt / 100, acc[3] / cnt / 100,
                acc[4] / cnt / 100, acc[5] / cnt / 100, acc[6] / cnt / 100);
+        {
+            double mloc = 0, late = 0, tot = 0;
+            for (int st = 1; st < SP; ++st)
+                for (int b = 0; b < G; ++b) {
+                    const uint64_t* q = &h[((size_t)b * SP + st) * PH];
+                    mloc += (double)(q[7] - q[1]);
+                    if (q[8]) { tot += 1; late += q[8] == 2; }
+                }
+            printf("sweep-done -> minloc-done %.2f us; winner row loaded after the sweep in %.0f%% of steps\n",
+                   mloc / ((SP - 1) * G) / 100, tot > 0 ? 100.0 * late / tot : -1.0);
+        }
         printf("compute split (us): register rows %.2f  LDS rows %.2f  streamed rows %.2f\n",
                acc[7] / cnt / 100, ph_lds / cnt / 100, (acc[0] - acc[7] - ph_lds) / cnt / 100);
     }
