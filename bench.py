@@ -209,10 +209,23 @@ def main():
         def run_once():
             prob.greedy_launch(m, idx, a, ws)
     else:
-        from stein_thinning.distributed import GraphedShardedGreedy, HipShardBackend, shard_bounds
-        r0, r1 = shard_bounds(n, rank, world)
-        backend = HipShardBackend(integrand, r0, r1, world, m)
-        runner = GraphedShardedGreedy(backend, m, use_graph=not args.no_graph)
+        from stein_thinning import distributed as sd
+        runner = None
+        exchange_note = ''
+        if world > 1 and sd.device_exchange_eligible(d, world):
+            mb = sd.peer_mailboxes()
+            if mb.ok:
+                runner = sd.PersistentShardedGreedy(integrand, rank, world, m, mb)
+                probe_idx = runner.run()     # validates the device exchange end to end (untimed)
+                if not mb._agree(runner.completed(probe_idx)):
+                    runner, exchange_note = None, 'device exchange timed out; '
+            else:
+                exchange_note = f'device exchange unavailable ({mb.error}); '
+        if runner is None:
+            r0, r1 = sd.shard_bounds(n, rank, world)
+            backend = sd.HipShardBackend(integrand, r0, r1, world, m)
+            runner = sd.GraphedShardedGreedy(backend, m, use_graph=not args.no_graph)
+            runner.mode = exchange_note + 'rccl-' + runner.mode
 
         def run_once():
             runner.launch()
@@ -243,7 +256,7 @@ def main():
     if not sharded:
         result_idx = idx.cpu().numpy().view(np.uint32)
     else:
-        result_idx = backend.indices()
+        result_idx = runner.indices() if hasattr(runner, 'indices') else runner.backend.indices()
 
     roofline = None
     cpu = None
@@ -300,7 +313,7 @@ def main():
             'data': 'synthetic (seeded RW-MH LV-surrogate chains; see bench.py docstring)',
             'config': {'workload': f"config {args.config[1]}: {cfg['desc']}", 'n': n, 'd': d, 'm': m,
                        'preconditioner': 'med', 'kernel': 'gradient-free' if integrand.weights is not None else 'langevin',
-                       'parallelism': (f'rows-sharded x{world}, RCCL record all-gather per step, {runner.mode}'
+                       'parallelism': (f'rows-sharded x{world}, per-step exchange: {runner.mode}'
                                        if sharded else 'single-gpu'),
                        'wallclock_thin_s': elapsed / args.steps,
                        'first_indices': result_idx[:8].tolist()},

@@ -143,6 +143,119 @@ int st_greedy(const double* x_soa, const double* g_soa, const double* weights, i
                            n_points, idx_out, a_work, workspace, workspace_bytes, stream);
 }
 
+int64_t st_mailbox_bytes(int32_t nranks) {
+    if (nranks < 1 || nranks > st::kMailboxRanks) return -1;
+    return st::kMailboxBytes;
+}
+
+int st_mailbox_alloc(int64_t bytes, void** mailbox) {
+    if (!mailbox || bytes < st::kMailboxBytes) return fail(ST_ERR_INVALID, "bad mailbox request");
+    *mailbox = nullptr;
+    // uncached device memory: peers' xGMI stores land in HBM and local polls never hit a stale
+    // L2 line
+    void* p = nullptr;
+    int rc = hip_check(hipExtMallocWithFlags(&p, (size_t)bytes, hipDeviceMallocUncached),
+                       "hipExtMallocWithFlags(uncached)");
+    if (rc) return rc;
+    rc = hip_check(hipMemset(p, 0, (size_t)bytes), "mailbox memset");
+    if (rc) { (void)hipFree(p); return rc; }
+    *mailbox = p;
+    return ST_OK;
+}
+
+int st_mailbox_free(void* mailbox) {
+    if (!mailbox) return ST_OK;
+    return hip_check(hipFree(mailbox), "hipFree(mailbox)");
+}
+
+int st_ipc_get_handle(void* dev_ptr, void* handle_out) {
+    if (!dev_ptr || !handle_out) return fail(ST_ERR_INVALID, "NULL pointer");
+    hipIpcMemHandle_t h;
+    int rc = hip_check(hipIpcGetMemHandle(&h, dev_ptr), "hipIpcGetMemHandle");
+    if (rc) return rc;
+    memcpy(handle_out, &h, sizeof(h));
+    return ST_OK;
+}
+
+int st_ipc_handle_bytes(void) { return (int)sizeof(hipIpcMemHandle_t); }
+
+int st_ipc_open_handle(const void* handle, void** dev_ptr) {
+    if (!handle || !dev_ptr) return fail(ST_ERR_INVALID, "NULL pointer");
+    hipIpcMemHandle_t h;
+    memcpy(&h, handle, sizeof(h));
+    *dev_ptr = nullptr;
+    return hip_check(hipIpcOpenMemHandle(dev_ptr, h, hipIpcMemLazyEnablePeerAccess),
+                     "hipIpcOpenMemHandle");
+}
+
+int st_ipc_close_handle(void* dev_ptr) {
+    if (!dev_ptr) return ST_OK;
+    return hip_check(hipIpcCloseMemHandle(dev_ptr), "hipIpcCloseMemHandle");
+}
+
+static int check_peers(void* const* peer_mailboxes, int32_t nranks, int32_t rank) {
+    if (nranks < 2 || nranks > st::kMailboxRanks)
+        return fail(ST_ERR_INVALID, "nranks must be in [2, %d]", st::kMailboxRanks);
+    if (rank < 0 || rank >= nranks) return fail(ST_ERR_INVALID, "rank out of range");
+    if (!peer_mailboxes) return fail(ST_ERR_INVALID, "NULL peer mailbox table");
+    for (int r = 0; r < nranks; ++r)
+        if (!peer_mailboxes[r] || !aligned16(peer_mailboxes[r]))
+            return fail(ST_ERR_INVALID, "peer mailbox %d is NULL or misaligned", r);
+    return ST_OK;
+}
+
+int st_mailbox_handshake(void* const* peer_mailboxes, int32_t nranks, int32_t rank,
+                         uint64_t token, int32_t* ok_device, void* stream) {
+    int rc = check_peers(peer_mailboxes, nranks, rank);
+    if (rc) return rc;
+    if (!ok_device) return fail(ST_ERR_INVALID, "NULL ok flag");
+    if (token >> 63) return fail(ST_ERR_INVALID, "token must be < 2^63");
+    st::MailboxPeers peers{};
+    for (int r = 0; r < nranks; ++r) peers.p[r] = static_cast<uint64_t*>(peer_mailboxes[r]);
+    return hip_check(st::launch_mailbox_handshake(peers, peers.p[rank], rank, nranks,
+                                                  token | (1ull << 63), ok_device,
+                                                  static_cast<hipStream_t>(stream)),
+                     "handshake launch");
+}
+
+int st_greedy_sharded(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
+                      int32_t d, int64_t ld, double linv_scale, double linv_trace,
+                      int64_t row_begin, int64_t row_end, int32_t rank, int32_t nranks,
+                      void* const* peer_mailboxes, uint64_t seq_base, int64_t n_points,
+                      uint32_t* idx_out, double* a_work, void* workspace,
+                      int64_t workspace_bytes, void* stream) {
+    if (n_points < 1) return fail(ST_ERR_INVALID, "n_points must be >= 1");
+    int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
+    if (rc) return rc;
+    rc = check_peers(peer_mailboxes, nranks, rank);
+    if (rc) return rc;
+    if (row_begin < 0 || row_end <= row_begin || row_end > n)
+        return fail(ST_ERR_INVALID, "need 0 <= row_begin < row_end <= n");
+    if (!idx_out || !a_work || !workspace) return fail(ST_ERR_INVALID, "NULL output/workspace");
+    if (!aligned16(a_work) || !aligned16(workspace))
+        return fail(ST_ERR_INVALID, "a_work/workspace must be 16-byte aligned");
+    if (workspace_bytes < greedy_ws_bytes(d))
+        return fail(ST_ERR_INVALID, "workspace too small (%lld < %lld)", (long long)workspace_bytes,
+                    (long long)greedy_ws_bytes(d));
+    st::RankSpec rs{};
+    rs.row_begin = row_begin;
+    rs.row_end = row_end;
+    rs.rank = rank;
+    rs.nranks = nranks;
+    rs.seq_base = seq_base;
+    rs.inbox = static_cast<uint64_t*>(peer_mailboxes[rank]);
+    for (int r = 0; r < nranks; ++r) rs.peer[r] = static_cast<uint64_t*>(peer_mailboxes[r]);
+    int used = 0;
+    const hipError_t e = st::launch_greedy_persistent(
+        x_soa, g_soa, weights, a_work, n, d, ld, linv_scale, linv_trace, n_points, idx_out, workspace,
+        workspace_bytes, static_cast<hipStream_t>(stream), &used, &rs);
+    if (used) return ST_OK;
+    if (e == hipErrorNotSupported)
+        return fail(ST_ERR_UNSUPPORTED, "multi-rank persistent kernel: d = %d not supported (d = 2, 4)", d);
+    (void)hipGetLastError();
+    return hip_check(e, "multi-rank persistent launch");
+}
+
 int st_greedy_step(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
                    int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t row_offset,
                    int64_t t, int32_t nranks, const double* cands_in, double* cand_out,

@@ -13,6 +13,13 @@
 //     writes idx.  Two record banks alternate by step parity.
 //   * Every spin is bounded by a wall-clock timeout (s_memrealtime); a timeout sets status[0] and
 //     every block leaves the step loop, so the grid always drains.
+// Multi-rank (one process per GPU, nranks > 1): every rank runs this kernel over its row block
+// [row_begin, row_end) of the full (replicated, read-only) arrays.  After the block-level sweep,
+// block 0 pushes the rank's winner {A_min, global index} as a 16-bit-tagged two-granule record
+// into slot `rank` of every peer's mailbox (IPC-mapped uncached device memory, system-scope
+// stores over xGMI); one wave per block polls the R slots of its own mailbox, loads each arriving
+// candidate's row from the replicated inputs, and picks the global winner in np.argmin order.
+// No host round trip and no collective launch per step.
 // Arithmetic per pair: K2's (stein_math.hpp) or, when the block's rows and the winner lie in the
 // guarded range, its division/sqrt-light form that returns the same bits (fast_div / fast_sqrt):
 // results are bit-identical to st_greedy's launch-per-step path and to the C bit model.
@@ -28,7 +35,9 @@ namespace {
 constexpr int kMaxPWaves = 8;                // up to 512-thread blocks
 constexpr int kShards = 8;
 constexpr int kMaxGrid = 256;               // one block per CU on MI355X (256 CUs)
+constexpr int kMaxRanks = kMailboxRanks;    // GPUs of one node
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
+constexpr uint64_t kFirstRankTimeoutTicks = 1000000000ull;   // 10 s: peers' launch skew at step 0
 
 __device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minloc(v, i); }
 
@@ -74,11 +83,11 @@ __device__ __forceinline__ double uniform(double v) {
 }  // namespace
 
 struct PersistArgs {
-    const double* x;
+    const double* x;      // SoA (d, ld), full sample (replicated on every rank)
     const double* g;
     const double* w;
-    double* A;
-    int64_t n, ld;
+    double* A;            // (ld) running sums; rows [row_begin, row_end) are this rank's
+    int64_t n, ld;        // n = total rows
     double l, tr;
     int64_t m;            // n_points
     uint32_t* idx_out;
@@ -87,6 +96,11 @@ struct PersistArgs {
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
     uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
+    int64_t row_begin, row_end;   // this rank's rows (global indices); one device: [0, n)
+    int rank, nranks;
+    uint64_t seq_base;            // exchange sequence number of step 0 (mailbox banks / tags)
+    uint64_t* inbox;              // this rank's mailbox (nranks > 1)
+    uint64_t* peer[kMaxRanks];    // every rank's mailbox as mapped in this process
 };
 
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
@@ -123,8 +137,10 @@ __device__ __forceinline__ uint64_t step_tag(int64_t t) { return (uint64_t)((t +
 
 template <int NT>
 __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, uint32_t row,
-                                        int64_t t) {
-    int64_t li = (int64_t)row;   // rows >= n (padding) carry +inf and never win
+                                        int64_t t, int64_t r1) {
+    // padding rows (>= r1) carry +inf and the "no row" sentinel index, so they lose every tie --
+    // their indices may be real rows of the next rank
+    int64_t li = (int64_t)row < r1 ? (int64_t)row : INT64_MAX;
     p_wave_minloc(v, li);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) { sc->v[wave] = v; sc->i[wave] = li; }
@@ -213,10 +229,70 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             }
         }
         ST_STAMP(a, t + 1, 1);
-        const int64_t my = gi;
+        int64_t my = gi;
         p_wave_minloc(v, gi);
         ST_STAMP(a, t + 1, 7);
-        // record indices are distinct across blocks, so exactly one lane holds the winner
+        if (a.nranks > 1 && ok_all) {
+            // ---- rank level: push this rank's winner to every peer, gather the R winners ----
+            const uint64_t seq = a.seq_base + (uint64_t)t;
+            const uint64_t rtag = ((seq + 1) & 0xFFFFull) << 48;
+            const int64_t mbank = (int64_t)(seq & 1) * kMaxRanks * 2;
+            const uint32_t lib = gi == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)gi;
+            if (blockIdx.x == 0 && lane == 0) {
+                const uint64_t vb = (uint64_t)__double_as_longlong(v);
+                const uint64_t g0 = rtag | (vb >> 16);
+                const uint64_t g1 = rtag | ((vb & 0xFFFFull) << 32) | lib;
+                for (int r = 0; r < a.nranks; ++r) {
+                    if (r == a.rank) continue;   // every block of this rank already has it
+                    uint64_t* dst = a.peer[r] + mbank + 2 * a.rank;
+                    __hip_atomic_store(dst + 0, g0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    __hip_atomic_store(dst + 1, g1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                }
+            }
+            // lane r < nranks owns rank r's record; lane `rank` holds the local winner already
+            double rv = INFINITY;
+            int64_t ri = INT64_MAX;
+            bool got = lane >= a.nranks;
+            if (lane == a.rank) {
+                rv = v;
+                ri = gi;
+                got = true;
+                if (ri != INT64_MAX && ri != row_of) { load_row(ri); row_of = ri; }
+            }
+            const uint64_t* slot = a.inbox + mbank + 2 * lane;
+            const uint64_t want16 = rtag;
+            const uint64_t limit = t == 0 ? kFirstRankTimeoutTicks : kTimeoutTicks;
+            const uint64_t t1 = __builtin_amdgcn_s_memrealtime();
+            for (unsigned it = 0;; ++it) {
+                if (!got) {
+                    const uint64_t g0 = __hip_atomic_load(slot + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    const uint64_t g1 = __hip_atomic_load(slot + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+                    if (((g0 & 0xFFFF000000000000ull) == want16) & ((g1 & 0xFFFF000000000000ull) == want16)) {
+                        got = true;
+                        rv = __longlong_as_double(
+                            (long long)(((g0 & 0x0000FFFFFFFFFFFFull) << 16) | ((g1 >> 32) & 0xFFFFull)));
+                        const uint32_t ib = (uint32_t)g1;
+                        ri = ib == 0xFFFFFFFFu ? INT64_MAX : (int64_t)ib;
+                        if (ri != INT64_MAX && ri < a.n) { load_row(ri); row_of = ri; }
+                    }
+                }
+                if (__all(got)) break;
+                __builtin_amdgcn_s_sleep(1);
+                if ((it & 15) == 15) {
+                    const bool late = __builtin_amdgcn_s_memrealtime() - t1 > limit;
+                    const bool other = __hip_atomic_load(a.status, __ATOMIC_RELAXED,
+                                                         __HIP_MEMORY_SCOPE_AGENT) != 0;
+                    if (__any(late || other)) { ok_all = 0; break; }
+                }
+            }
+            my = ri;
+            v = rv;
+            gi = ri;
+            p_wave_minloc(v, gi);
+            // a record's index is never past n (a peer's padding sentinel is INT64_MAX)
+            if (gi != INT64_MAX && gi >= a.n) ok_all = 0;
+        }
+        // record indices are distinct across blocks (and ranks), so exactly one lane holds the winner
         if (ok_all && my == gi && gi != INT64_MAX) {
 #ifdef ST_PERSIST_STAMPS
             if (a.stamps && t + 1 >= kStampFirst && t + 1 < kStampFirst + kStampSteps)
@@ -251,8 +327,8 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
     double* sw = sa + RL;                                     // [RL] (GF)
     const int tid = threadIdx.x;
     const int64_t ld = a.ld;
-    const int64_t r0 = (int64_t)blockIdx.x * a.rows_per_block;
-    const int64_t r1 = (r0 + a.rows_per_block < a.n) ? r0 + a.rows_per_block : a.n;
+    const int64_t r0 = a.row_begin + (int64_t)blockIdx.x * a.rows_per_block;
+    const int64_t r1 = (r0 + a.rows_per_block < a.row_end) ? r0 + a.rows_per_block : a.row_end;
     const int64_t lds_base = r0 + (int64_t)RT * kPBlock;
     const int64_t str_base = lds_base + RL;
     const double l = a.l, l2 = a.l * a.l, tr = a.tr;
@@ -326,7 +402,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         a.A[row] = kv;
         scan_take(kv, (uint32_t)row, bv, bi);
     }
-    publish<NT>(a, sc, bv, bi, 0);
+    publish<NT>(a, sc, bv, bi, 0, r1);
 
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
     int64_t t = 1;
@@ -452,7 +528,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
         if (__builtin_amdgcn_readfirstlane(wfast)) sweep_rows(std::true_type{});
         else sweep_rows(std::false_type{});
         ST_STAMP(a, t, 3);
-        publish<NT>(a, sc, bv, bi, t);
+        publish<NT>(a, sc, bv, bi, t, r1);
         ST_STAMP(a, t, 4);
     }
     int64_t done = t;   // idx[0 .. done-1) are written
@@ -490,6 +566,7 @@ int64_t persistent_ws_bytes(int d, int G) {
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
 static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (256)
+static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (one per CU)
 static uint64_t* g_stamps = nullptr;
 #ifdef ST_PERSIST_STAMPS
 extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
@@ -505,6 +582,11 @@ int persistent_tune(int key, int value) {
         g_persist_nt = value;
         return 0;
     }
+    if (key == 5) {
+        if (value < -1 || value == 0 || value > kMaxGrid) return -1;
+        g_persist_grid = value;
+        return 0;
+    }
     return -1;
 }
 
@@ -516,6 +598,12 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     if (e != hipSuccess) return e;
     PersistArgs args = a;
     void* kargs[] = {&args};
+    // one device: cooperative launch (co-residency checked at launch).  Several ranks: a plain
+    // launch of the same one-block-per-CU grid (same residency, MI355X_MICROARCH.md coop-launch
+    // row), so that ranks sharing a device in tests are not serialised by the cooperative queue;
+    // a rank that cannot make progress times out, it never hangs.
+    if (a.nranks > 1)
+        return hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs, lds, s);
     return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs,
                                       lds, s);
 }
@@ -538,11 +626,18 @@ static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int G, size_
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
-                                    int* used) {
+                                    int* used, const RankSpec* rs) {
     *used = 0;
+    const RankSpec one{0, n, 0, 1, 0, nullptr, {}};
+    if (!rs) rs = &one;
     // 32-bit row indices, padding rows included (< n + one block's register rows)
     if (g_persist_rt == 0 || (d != 2 && d != 4) || m < 1 || m >= 0xFFFFFFFFll || n >= 0x7FFFFFFFll)
         return hipErrorNotSupported;
+    if (rs->nranks < 1 || rs->nranks > kMaxRanks || rs->rank < 0 || rs->rank >= rs->nranks ||
+        rs->row_begin < 0 || rs->row_end <= rs->row_begin || rs->row_end > n ||
+        (rs->nranks > 1 && !rs->inbox))
+        return hipErrorInvalidValue;
+    const int64_t n_shard = rs->row_end - rs->row_begin;
     int dev = 0, cus = 0, lds_max = 0, lds_optin = 0, coop = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -556,11 +651,12 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         lds_max = lds_optin;
     if (lds_max > 163840) lds_max = 163840;
     int G = cus > kMaxGrid ? kMaxGrid : cus;
+    if (g_persist_grid > 0 && G > g_persist_grid) G = g_persist_grid;
     const int64_t min_rows = 256;   // fewer blocks for small n: exchange cost grows with G
-    if (n < (int64_t)G * min_rows) G = (int)((n + min_rows - 1) / min_rows);
+    if (n_shard < (int64_t)G * min_rows) G = (int)((n_shard + min_rows - 1) / min_rows);
     if (G < 1) G = 1;
     if (persistent_ws_bytes(d, G) > ws_bytes) return hipErrorNotSupported;
-    const int64_t R = (n + G - 1) / G;
+    const int64_t R = (n_shard + G - 1) / G;
     const int nt = g_persist_nt > 0 ? g_persist_nt : 256;
     const int rt_max = nt == 512 ? 8 : 16;
     int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
@@ -589,6 +685,13 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.rows_per_block = R;
     a.RL = (int)RL;
     a.stamps = g_stamps;
+    a.row_begin = rs->row_begin;
+    a.row_end = rs->row_end;
+    a.rank = rs->rank;
+    a.nranks = rs->nranks;
+    a.seq_base = rs->seq_base;
+    a.inbox = rs->inbox;
+    for (int r = 0; r < kMaxRanks; ++r) a.peer[r] = r < rs->nranks ? rs->peer[r] : nullptr;
     // zero status and every granule tag (a stale tag from a previous run must never match)
     hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G), s);
     if (e != hipSuccess) return e;
@@ -598,5 +701,37 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     return e;
 }
 
+// ------------------------------------------------------------------------------------------
+// mailbox: [2 banks x kMaxRanks slots x 2 granules][kMaxRanks handshake words], u64
+// ------------------------------------------------------------------------------------------
+__global__ void mailbox_handshake(MailboxPeers peers, uint64_t* inbox, int rank, int nranks,
+                                  uint64_t token, int* ok) {
+    const int lane = threadIdx.x;
+    if (lane == 0)
+        for (int r = 0; r < nranks; ++r)
+            __hip_atomic_store(peers.p[r] + kMailboxHandshake + rank, token, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_SYSTEM);
+    bool got = lane >= nranks;
+    const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    int good = 1;
+    for (unsigned it = 0;; ++it) {
+        if (!got)
+            got = __hip_atomic_load(inbox + kMailboxHandshake + lane, __ATOMIC_RELAXED,
+                                    __HIP_MEMORY_SCOPE_SYSTEM) == token;
+        if (__all(got)) break;
+        __builtin_amdgcn_s_sleep(2);
+        if ((it & 15) == 15 && __any(__builtin_amdgcn_s_memrealtime() - t0 > kFirstRankTimeoutTicks)) {
+            good = 0;
+            break;
+        }
+    }
+    if (lane == 0) ok[0] = good;
+}
+
+hipError_t launch_mailbox_handshake(const MailboxPeers& peers, uint64_t* inbox, int rank,
+                                    int nranks, uint64_t token, int* ok, hipStream_t s) {
+    hipLaunchKernelGGL(mailbox_handshake, dim3(1), dim3(64), 0, s, peers, inbox, rank, nranks, token, ok);
+    return hipGetLastError();
+}
 
 }  // namespace st

@@ -10,6 +10,25 @@ constexpr int kMaxCtDim = 8;     // compile-time-d kernels for d <= 8
 constexpr int kMaxBlocks = 1024; // greedy step grid cap (4 x 256-thread blocks per CU)
 constexpr int kCandHeader = 2;   // candidate record: {val, gidx(bits)} then x[d], g[d], w
 constexpr int64_t kWsControlBytes = 8 * 128 + 128;   // persistent kernel: arrival counters + status
+// peer mailbox of the multi-rank persistent kernel (u64 words): 2 banks x kMailboxRanks slots x
+// 2 granules, then kMailboxRanks handshake words
+constexpr int kMailboxRanks = 8;
+constexpr int kMailboxHandshake = 2 * kMailboxRanks * 2;
+constexpr int64_t kMailboxBytes = 512;
+static_assert((kMailboxHandshake + kMailboxRanks) * 8 <= kMailboxBytes, "mailbox layout");
+
+struct MailboxPeers {
+    uint64_t* p[kMailboxRanks];
+};
+
+// row block and peers of one rank of a multi-GPU persistent run (nranks == 1: one device)
+struct RankSpec {
+    int64_t row_begin, row_end;
+    int rank, nranks;
+    uint64_t seq_base;
+    uint64_t* inbox;
+    uint64_t* peer[kMailboxRanks];
+};
 
 inline int64_t cand_stride(int d) { return ((kCandHeader + 2 * d + 1) + 1) & ~int64_t(1); }
 
@@ -39,7 +58,9 @@ int64_t persistent_ws_bytes(int d, int G);
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
-                                    int* used);
+                                    int* used, const RankSpec* ranks = nullptr);
+hipError_t launch_mailbox_handshake(const MailboxPeers& peers, uint64_t* inbox, int rank,
+                                    int nranks, uint64_t token, int* ok, hipStream_t s);
 hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStream_t s);
 hipError_t launch_greedy_publish(const double* recs, int K, int64_t stride, int d, double* out,
                                  hipStream_t s);

@@ -51,6 +51,17 @@ SIGNATURES = {
     'st_kmat': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i64, _i32, _f64, _f64, _c_dp,
                                _c_dp]),
     'st_layout_soa': (ctypes.c_int, [_c_dp, _i64, _i32, _i64, _c_dp, _c_dp]),
+    'st_mailbox_bytes': (_i64, [_i32]),
+    'st_mailbox_alloc': (ctypes.c_int, [_i64, ctypes.POINTER(ctypes.c_void_p)]),
+    'st_mailbox_free': (ctypes.c_int, [_c_dp]),
+    'st_ipc_handle_bytes': (ctypes.c_int, []),
+    'st_ipc_get_handle': (ctypes.c_int, [_c_dp, _c_dp]),
+    'st_ipc_open_handle': (ctypes.c_int, [_c_dp, ctypes.POINTER(ctypes.c_void_p)]),
+    'st_ipc_close_handle': (ctypes.c_int, [_c_dp]),
+    'st_mailbox_handshake': (ctypes.c_int, [_c_dp, _i32, _i32, ctypes.c_uint64, _c_dp, _c_dp]),
+    'st_greedy_sharded': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
+                                         _i64, _i64, _i32, _i32, _c_dp, ctypes.c_uint64, _i64,
+                                         _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
 }
 ABI_VERSION = 1
 

@@ -1,20 +1,29 @@
-"""Row-sharded greedy Stein thinning across GPUs (one process per GPU, RCCL over xGMI).
+"""Row-sharded greedy Stein thinning across GPUs (one process per GPU of one node, over xGMI).
 
 The reference has no multi-device path (its only parallelism is joblib / Dask fan-out over chains,
 ``code/src/utils/parallel.py:18-52``).  Here the candidate axis n of one greedy run is split into
-contiguous row blocks, one per rank.  Per step every rank streams its shard (fused kernel), reduces
-it to ONE candidate record {value, global index, x row, g row, w} and the ranks all-gather those
-records (``8 * stride`` bytes per rank; RCCL ``all_gather_into_tensor``).  Every rank then picks the
-same winner (lowest value, then lowest global index, NaN first: np.argmin over the concatenated
-array) at the start of its next kernel.  No n-length vector ever crosses xGMI; the design choice
-vs. an all-reduce of the n-length column-sum vector is recorded in DESIGN.md.
+contiguous row blocks, one per rank; every rank picks the same winner per step (lowest value, then
+lowest global index, NaN first: np.argmin over the concatenated array).  Two exchange engines:
+
+* ``PersistentShardedGreedy`` (d = 2, 4; default): every rank holds the full standardised arrays
+  (replicated, read-only) and runs ONE persistent launch over its row block; per step the ranks
+  exchange their local winners {A_min, global index} through IPC-mapped device mailboxes (xGMI
+  stores, no host round trip, no collective launch).  Handles are exchanged once with
+  ``torch.distributed`` and the round trip is verified by a handshake before first use.
+* ``GraphedShardedGreedy`` (any d; fallback): per step a fused kernel over the shard, ONE candidate
+  record {value, global index, x row, g row, w} per rank, RCCL ``all_gather_into_tensor`` of the
+  records, the m-step loop captured once into a HIP graph.
+
+No n-length vector crosses xGMI in either; the design choice vs. an all-reduce of the n-length
+column-sum vector is recorded in DESIGN.md (that all-reduce is used by the full-sample KSD).
 
 Each rank passes the FULL host arrays: standardisation and the 'med' preconditioner are computed
-from all rows exactly as the single-process reference does (bit-identical), then only the rank's
-shard is uploaded.
+from all rows exactly as the single-process reference does (bit-identical).
 """
 from __future__ import annotations
 
+import ctypes
+import os
 from typing import Optional
 
 import numpy as np
@@ -150,6 +159,166 @@ class GraphedShardedGreedy:
         return self.backend.indices()
 
 
+MAX_PEER_RANKS = 8   # mailbox table size (include/stein_thinning_hip.h: one node)
+
+
+class PeerMailboxes:
+    """This rank's device mailbox plus its peers' mailboxes mapped into this process (IPC).
+
+    Created collectively by every rank of ``group``; ``ok`` is the group-wide verdict (IPC setup
+    and a device-side handshake succeeded on EVERY rank).  ``seq`` is the exchange sequence
+    number the next persistent run starts at (identical on every rank: all ranks run the same
+    sequence of collective thins)."""
+
+    def __init__(self, group=None):
+        import torch
+        import torch.distributed as dist
+        self.group = group
+        self.rank, self.world = dist.get_rank(group), dist.get_world_size(group)
+        self.device = nat.require_device()
+        self.seq = 0
+        self.token = 0
+        self.local = ctypes.c_void_p()
+        self.opened = []
+        self.table = (ctypes.c_void_p * MAX_PEER_RANKS)()
+        L = nat.lib()
+        err = ''
+        handle = b''
+        try:
+            if self.world > MAX_PEER_RANKS:
+                raise ValueError(f'{self.world} ranks > {MAX_PEER_RANKS}')
+            nat.check(L.st_mailbox_alloc(L.st_mailbox_bytes(self.world), ctypes.byref(self.local)),
+                      'st_mailbox_alloc')
+            hb = L.st_ipc_handle_bytes()
+            h = (ctypes.c_ubyte * hb)()
+            nat.check(L.st_ipc_get_handle(self.local, h), 'st_ipc_get_handle')
+            handle = bytes(h)
+        except Exception as e:   # noqa: BLE001 -- reported through the group verdict
+            err = f'{type(e).__name__}: {e}'
+        handles = [None] * self.world
+        dist.all_gather_object(handles, handle, group=group)
+        if not err and all(handles):
+            try:
+                for r in range(self.world):
+                    if r == self.rank:
+                        self.table[r] = self.local.value
+                        continue
+                    p = ctypes.c_void_p()
+                    hr = (ctypes.c_ubyte * len(handles[r])).from_buffer_copy(handles[r])
+                    nat.check(L.st_ipc_open_handle(hr, ctypes.byref(p)), f'st_ipc_open_handle(rank {r})')
+                    self.opened.append(p)
+                    self.table[r] = p.value
+            except Exception as e:   # noqa: BLE001
+                err = f'{type(e).__name__}: {e}'
+        elif not err:
+            err = 'a peer failed to export its mailbox'
+        self.error = err
+        self.ok = self._agree(not err) and self.handshake()
+
+    def _agree(self, flag: bool) -> bool:
+        """Group-wide AND of a per-rank flag."""
+        import torch
+        import torch.distributed as dist
+        dev = self.device if dist.get_backend(self.group) == 'nccl' else torch.device('cpu')
+        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
+        return bool(int(t.item()))
+
+    def handshake(self) -> bool:
+        """Every rank stores a token into every peer's mailbox and polls its own (device side,
+        bounded wait); True iff all ranks saw all tokens."""
+        import torch
+        self.token += 1
+        ok = torch.zeros(1, dtype=torch.int32, device=self.device)
+        good = False
+        try:
+            nat.check(nat.lib().st_mailbox_handshake(ctypes.cast(self.table, ctypes.c_void_p), self.world,
+                                                     self.rank, self.token, nat.ptr(ok),
+                                                     nat.stream_handle()), 'st_mailbox_handshake')
+            torch.cuda.synchronize()
+            good = int(ok.item()) == 1
+            if not good:
+                self.error = 'mailbox handshake timed out'
+        except Exception as e:   # noqa: BLE001
+            self.error = f'{type(e).__name__}: {e}'
+        return self._agree(good)
+
+    def table_ptr(self):
+        return ctypes.cast(self.table, ctypes.c_void_p)
+
+    def close(self) -> None:
+        L = nat.lib()
+        for p in self.opened:
+            L.st_ipc_close_handle(p)
+        self.opened = []
+        if self.local.value:
+            L.st_mailbox_free(self.local)
+            self.local = ctypes.c_void_p()
+        self.ok = False
+
+
+_MAILBOXES = {}
+
+
+def peer_mailboxes(group=None) -> PeerMailboxes:
+    """The process-wide mailbox set of ``group`` (collective on first use)."""
+    import torch.distributed as dist
+    key = (id(group), dist.get_world_size(group), dist.get_rank(group))
+    mb = _MAILBOXES.get(key)
+    if mb is None:
+        mb = _MAILBOXES[key] = PeerMailboxes(group)
+    return mb
+
+
+def device_exchange_eligible(d: int, world: int) -> bool:
+    """Whether the persistent multi-rank kernel serves this run (ST_SHARDED_EXCHANGE=rccl forces
+    the RCCL path)."""
+    return (d in (2, 4) and 2 <= world <= MAX_PEER_RANKS
+            and os.environ.get('ST_SHARDED_EXCHANGE', 'device') != 'rccl')
+
+
+class PersistentShardedGreedy:
+    """One rank of a multi-GPU greedy run on the persistent kernel with device-side exchange
+    (C-ABI ``st_greedy_sharded``).  The full standardised problem is resident on every rank; this
+    rank sweeps rows [r0, r1)."""
+
+    mode = 'device-exchange'
+
+    def __init__(self, integrand: SteinIntegrand, rank: int, world: int, n_points: int,
+                 mailboxes: PeerMailboxes, problem=None):
+        from .device import DeviceProblem
+        self.device = nat.require_device()
+        self.prob = problem if problem is not None else DeviceProblem(
+            integrand.sample, integrand.gradient, integrand.weights, integrand.linv_scale,
+            integrand.linv_trace, self.device)
+        self.rank, self.world, self.n_points = rank, world, int(n_points)
+        self.r0, self.r1 = shard_bounds(self.prob.n, rank, world)
+        self.mb = mailboxes
+        self.idx, self.a, self.ws = self.prob.greedy_buffers(self.n_points)
+
+    def launch(self) -> None:
+        """Enqueue one whole greedy run on the current stream (collective: every rank calls it)."""
+        p = self.prob
+        seq = self.mb.seq
+        self.mb.seq += self.n_points
+        nat.check(nat.lib().st_greedy_sharded(
+            nat.ptr(p.x), nat.ptr(p.g), nat.ptr(p.w), p.n, p.d, p.ld, p.l, p.tr, self.r0, self.r1,
+            self.rank, self.world, self.mb.table_ptr(), seq, self.n_points, nat.ptr(self.idx),
+            nat.ptr(self.a), nat.ptr(self.ws), self.ws.numel() * 8, nat.stream_handle()),
+            'st_greedy_sharded')
+
+    def indices(self) -> np.ndarray:
+        return self.idx.cpu().numpy().view(np.uint32).copy()
+
+    def completed(self, idx: Optional[np.ndarray] = None) -> bool:
+        idx = self.indices() if idx is None else idx
+        return bool(idx.size == 0 or int(idx.max()) < self.prob.n)
+
+    def run(self) -> np.ndarray:
+        self.launch()
+        return self.indices()
+
+
 def _world(group):
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized():
@@ -179,9 +348,26 @@ def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None
     rank, world = _world(group)
     if world > integrand.n:
         raise ValueError(f'{world} ranks for {integrand.n} rows: every rank needs at least one row')
+    global last_mode
+    import torch.distributed as dist
+    if world > 1 and device_exchange_eligible(integrand.sample.shape[1], world):
+        mb = peer_mailboxes(group)
+        if mb.ok:
+            runner = PersistentShardedGreedy(integrand, rank, world, n_points, mb)
+            idx = runner.run()
+            if mb._agree(runner.completed(idx)):
+                last_mode = runner.mode
+                return idx
+            mb.ok = False   # a bounded wait expired somewhere: RCCL path from now on
+            mb.error = 'persistent run timed out'
     r0, r1 = shard_bounds(integrand.n, rank, world)
     backend = HipShardBackend(integrand, r0, r1, world, n_points)
-    import torch.distributed as dist
     if dist.is_initialized() and dist.get_backend(group) == 'nccl':
-        return GraphedShardedGreedy(backend, n_points, group, use_graph).run()
+        runner = GraphedShardedGreedy(backend, n_points, group, use_graph)
+        last_mode = f'rccl-{runner.mode}'
+        return runner.run()
+    last_mode = 'records-all-gather'
     return run_sharded(backend, n_points, group)
+
+
+last_mode = None   # exchange engine of the last sharded thin in this process (tests / bench)

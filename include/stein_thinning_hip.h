@@ -10,7 +10,8 @@
  * Conventions (all functions):
  *   - plain C types only; device pointers are HIP device memory owned by the caller;
  *   - `stream` is a hipStream_t (NULL = default stream); every function is asynchronous on it,
- *     allocates nothing and never synchronises (graph-capturable);
+ *     allocates nothing and never synchronises (graph-capturable) -- except the one-time
+ *     multi-GPU setup calls st_mailbox_alloc / st_mailbox_free / st_ipc_*, which are synchronous;
  *   - sample / gradient arrays are SoA: element (i, k) of the (n, d) array lives at p[k * ld + i],
  *     ld a multiple of 8 and >= n; per-row arrays (weights, running sums) have ld entries (rows
  *     n..ld-1 are padding: read, and in the running sums overwritten, never selected);
@@ -57,7 +58,8 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * (1, 2, 4; d = 2 and 4 kernels; -1 = automatic), key 2 = register prefetch of the next tile
  * (0/1; -1 = automatic), key 3 = persistent kernel register rows per thread (4, 8, 16;
  * -1 = automatic, 0 = disable the persistent kernel), key 4 = persistent kernel threads per
- * block (256, 512; -1 = automatic).
+ * block (256, 512; -1 = automatic), key 5 = persistent kernel grid cap (blocks per device,
+ * 1..256; -1 = one per CU).
  */
 int st_tune(int32_t key, int32_t value);
 
@@ -106,6 +108,38 @@ int st_greedy_step(const double *x_soa, const double *g_soa, const double *weigh
 
 int st_greedy_finalize(const double *cands_in, int32_t nranks, int32_t d, uint32_t *idx_out,
                        int64_t t, void *stream);
+
+/* ------------------------------------------------------------------------------------------
+ * Multi-GPU greedy with device-side exchange (one process per GPU of one node, up to 8).
+ * Same result as st_greedy on the whole sample (and as the reference's _greedy_search).
+ *
+ * Every rank holds the FULL standardised arrays (replicated, read-only: the winner's row is then
+ * local) and runs ONE persistent launch over its row block [row_begin, row_end).  Per step the
+ * ranks exchange their local winners {A_min, global index} through per-rank mailboxes: each rank
+ * allocates one (st_mailbox_alloc: uncached device memory), exports it (st_ipc_get_handle), the
+ * handles are all-gathered out of band (torch.distributed), each rank maps its peers'
+ * (st_ipc_open_handle) and passes the table peer_mailboxes[0..nranks) (its own at [rank]).
+ * st_mailbox_handshake verifies the round trip (ok_device[0] = 1) before the first run.
+ * seq_base: exchange sequence number of this run's step 0; every rank passes the same value and
+ * a following run on the same mailboxes uses seq_base + n_points.
+ * Returns ST_ERR_UNSUPPORTED when d is not 2 or 4 (use st_greedy_step + RCCL instead); a run
+ * whose peers do not answer within the kernel's bounded waits poisons idx_out (UINT32_MAX).
+ * ---------------------------------------------------------------------------------------- */
+int64_t st_mailbox_bytes(int32_t nranks);
+int st_mailbox_alloc(int64_t bytes, void **mailbox);
+int st_mailbox_free(void *mailbox);
+int st_ipc_handle_bytes(void);
+int st_ipc_get_handle(void *dev_ptr, void *handle_out);
+int st_ipc_open_handle(const void *handle, void **dev_ptr);
+int st_ipc_close_handle(void *dev_ptr);
+int st_mailbox_handshake(void *const *peer_mailboxes, int32_t nranks, int32_t rank,
+                         uint64_t token, int32_t *ok_device, void *stream);
+int st_greedy_sharded(const double *x_soa, const double *g_soa, const double *weights, int64_t n,
+                      int32_t d, int64_t ld, double linv_scale, double linv_trace,
+                      int64_t row_begin, int64_t row_end, int32_t rank, int32_t nranks,
+                      void *const *peer_mailboxes, uint64_t seq_base, int64_t n_points,
+                      uint32_t *idx_out, double *a_work, void *workspace,
+                      int64_t workspace_bytes, void *stream);
 
 /* ------------------------------------------------------------------------------------------
  * Integrand protocol -- replaces integrand(ind1, ind2) of the closures returned by

@@ -37,33 +37,57 @@ def _data():
     return x, g, log_p, log_q
 
 
-def _worker(rank, world, port, backend, gf, out_dir):
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+def _worker(rank, world, port, backend, gf, out_dir, exchange='device', runs=1):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE=exchange)
     torch.cuda.set_device(0)
     kw = dict(device_id=torch.device('cuda', 0)) if backend == 'nccl' else {}
     dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     try:
-        from stein_thinning.distributed import thin_gf_sharded, thin_sharded
+        from stein_thinning import distributed as sd
         x, g, log_p, log_q = _data()
-        if gf:
-            idx = thin_gf_sharded(x, log_p, log_q, g, 80, preconditioner='med')
-        else:
-            idx = thin_sharded(x, g, 80, preconditioner='med')
-        np.save(os.path.join(out_dir, f'idx{rank}.npy'), idx)
+        for run in range(runs):
+            gf_run = gf if run % 2 == 0 else not gf   # alternate kernels on the same mailboxes
+            if gf_run:
+                idx = sd.thin_gf_sharded(x, log_p, log_q, g, 80, preconditioner='med')
+            else:
+                idx = sd.thin_sharded(x, g, 80, preconditioner='med')
+            np.save(os.path.join(out_dir, f'idx{rank}_{run}.npy'), idx)
+            with open(os.path.join(out_dir, f'mode{rank}_{run}.txt'), 'w') as f:
+                f.write(str(sd.last_mode))
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize('gf', [False, True])
-def test_two_processes_one_gpu_gloo(tmp_path, gf):
-    mp.spawn(_worker, args=(2, _free_port(), 'gloo', gf, str(tmp_path)), nprocs=2, join=True)
+def _want(gf):
     x, g, log_p, log_q = _data()
-    want = o.thin_gf(x, log_p, log_q, g, 80, preconditioner='med') if gf else o.thin(x, g, 80, preconditioner='med')
+    return o.thin_gf(x, log_p, log_q, g, 80, preconditioner='med') if gf else o.thin(x, g, 80, preconditioner='med')
+
+
+@pytest.mark.parametrize('gf', [False, True])
+def test_two_processes_one_gpu_gloo_rccl_records(tmp_path, gf):
+    """Per-step record all-gather path (forced), two ranks exchanging through gloo."""
+    mp.spawn(_worker, args=(2, _free_port(), 'gloo', gf, str(tmp_path), 'rccl'), nprocs=2, join=True)
+    want = _want(gf)
     for r in range(2):
-        np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}.npy'), want)
+        np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_0.npy'), want)
+        assert (tmp_path / f'mode{r}_0.txt').read_text() == 'records-all-gather'
+
+
+@pytest.mark.parametrize('world,gf', [(2, False), (3, True)])
+def test_device_exchange_processes_share_one_gpu(tmp_path, world, gf):
+    """Persistent multi-rank kernel: `world` processes on the one visible GPU, IPC-mapped device
+    mailboxes (the same code path as one rank per GPU over xGMI), three consecutive runs on the
+    same mailboxes (sequence numbers / tags carry over), both kernels."""
+    mp.spawn(_worker, args=(world, _free_port(), 'gloo', gf, str(tmp_path), 'device', 3), nprocs=world,
+             join=True)
+    for run in range(3):
+        want = _want(gf if run % 2 == 0 else not gf)
+        for r in range(world):
+            assert (tmp_path / f'mode{r}_{run}.txt').read_text() == 'device-exchange'
+            np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
 
 
 def test_single_rank_rccl_graph_capture(tmp_path):
     mp.spawn(_worker, args=(1, _free_port(), 'nccl', False, str(tmp_path)), nprocs=1, join=True)
     x, g, _, _ = _data()
-    np.testing.assert_array_equal(np.load(tmp_path / 'idx0.npy'), o.thin(x, g, 80, preconditioner='med'))
+    np.testing.assert_array_equal(np.load(tmp_path / 'idx0_0.npy'), o.thin(x, g, 80, preconditioner='med'))
