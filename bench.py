@@ -5,8 +5,11 @@ A "step" = one complete greedy thin of the HBM-resident standardised sample (dia
 kernel steps + argmin), i.e. n*m pair-evals; ms_per_step is the wall-clock of one thin.
 N = 1 workload: config 4 of BASELINE.json (LV surrogate, d=4, n=2e6, Langevin IMQ, 'med', m=1000),
 one launch of the persistent on-chip-resident kernel per thin (csrc/persistent.hip).
-N > 1 (torchrun, one rank per GPU, RCCL): the same n rows sharded across ranks (strong scaling),
-one 16-B-per-rank-candidate all-gather per step.
+N > 1 (torchrun, one rank per GPU): the same n rows sharded across ranks (strong scaling); d = 2, 4:
+one persistent launch per rank per thin, the ranks' per-step winners exchanged through IPC-mapped
+device mailboxes over xGMI (stein_thinning/distributed.py PersistentShardedGreedy); other d (or if
+the device exchange is unavailable): per-step kernels + RCCL all-gather of the rank records, the loop
+captured in a HIP graph.  The mode used is reported in config.parallelism.
 
 Synthetic data (no network): the LV posterior chains of the reference live only in S3, so the
 "LV surrogate" is a seeded random-walk Metropolis chain on N(mu, Sigma) with mu, Sigma the
@@ -260,39 +263,76 @@ def main():
 
     roofline = None
     cpu = None
-    if rank == 0:
-        bytes_per_pair = 16 * d + (24 if integrand.weights is not None else 16)
-        flop_per_pair = 12 * d + 40            # ~90 flop per pair at d = 4
+    persistent = d in (2, 4) and (not sharded or runner.mode == 'device-exchange')
+    if rank == 0 or sharded:
+        gf = integrand.weights is not None
+        bytes_per_pair = 16 * d + (24 if gf else 16)
+        # fp64 work per pair of the persistent kernel's hot loop, counted in its ISA
+        # (greedy_persistent<4,false,16,256>, range-guarded variant): 38 v_mul_f64 + 26 v_add_f64
+        # + 33 v_fma/v_fmac_f64 + 3 v_rcp_f64 + 1 v_rsq_f64 = 101 fp64 VALU instructions,
+        # 134 flop (fma = 2); each further coordinate adds 13 (2 sub, 6 mul, 3 add, 1 mul + 1 add
+        # of the score product); the gradient-free weights add 2 mul
+        instr_per_pair = 101 + 13 * (d - 4) + (2 if gf else 0)
+        flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0)
         pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
         pmc_rec = json.load(open(pmc)) if os.path.exists(pmc) else {}
-        if not sharded:
-            # dominant kernel = the single persistent launch that runs the whole thin; its duration
-            # = HIP events on the launch stream around each timed thin (includes the ~2 us
-            # workspace memset enqueued just before it)
-            avg, med = float(np.mean(launch_s)), float(np.median(launch_s))
-            alg_bytes = n * m * bytes_per_pair
-            achieved = alg_bytes / avg / 1e9
-            rec = pmc_rec.get(f'{args.config}_persistent')
+        if persistent:
+            # dominant kernel = the single persistent launch that runs the whole thin (per rank);
+            # its duration = HIP events on the launch stream around each timed thin (includes the
+            # ~2 us workspace memset enqueued just before it); max over ranks
+            avg = float(np.mean(launch_s))
+            med = float(np.median(launch_s))
+            if sharded:
+                import torch
+                tt = torch.tensor([avg, med], dtype=torch.float64, device=dev)
+                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+                avg, med = (float(v) for v in tt.tolist())
+            pairs_launch = n * m / world          # per rank
+            tflops = pairs_launch * flop_per_pair / avg / 1e12
+            gins = pairs_launch * instr_per_pair / avg / 1e12
+            issue_peak = 256 * 4 * 16 * 2.4e9 / 1e12   # fp64 lane-instructions/s (T), 4 cycles per wave-instr
+            alg_bytes = int(pairs_launch * bytes_per_pair)
+            rec = pmc_rec.get(f'{args.config}_persistent') if world == 1 else None
             traffic = round(rec['hbm_bytes_per_launch']) if rec else None
-            tflops = n * m * flop_per_pair / avg / 1e12
-            roofline = {'bound': 'hbm', 'achieved': round(achieved, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                        'frac': round(achieved / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                        'kernel': f'greedy_persistent<{d},{str(integrand.weights is not None).lower()},RT,256>',
-                        'kernel_avg_us': round(avg * 1e6, 1), 'kernel_median_us': round(med * 1e6, 1),
-                        'timing': f'HIP events on the launch stream around each of the {args.steps} timed thins',
-                        'algorithmic_bytes_per_launch': alg_bytes, 'bytes_per_pair': bytes_per_pair,
-                        'note': ('algorithmic bytes = SURVEY 8(d) streaming figure (n*m*B_pair); the persistent '
-                                 'kernel keeps most rows in VGPR/AGPR/LDS across steps, so measured HBM traffic '
-                                 '(PMC) is far below it and the binding roofline is fp64 VALU issue (valu_fp64)'),
-                        'valu_fp64': {'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
-                                      'frac': round(tflops / FP64_VALU_PEAK_TFS, 4),
-                                      'flop_per_pair': flop_per_pair}}
-            if not args.no_kernel_timing:
-                s_avg, s_med = kernel_timing(prob, min(m, 200))
-                roofline['step_kernel'] = {
-                    'kernel': f'greedy_step_ct<{d}> (launch-per-step path, st_greedy_steps)',
-                    'avg_us': round(s_avg * 1e6, 2), 'median_us': round(s_med * 1e6, 2),
-                    'achieved_GBs': round(n * bytes_per_pair / s_avg / 1e9, 1)}
+            roofline = {
+                'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
+                'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': traffic,
+                'kernel': f'greedy_persistent<{d},{str(gf).lower()},RT,256>' + (f' x{world} ranks' if sharded else ''),
+                'kernel_avg_us': round(avg * 1e6, 1), 'kernel_median_us': round(med * 1e6, 1),
+                'timing': f'HIP events on the launch stream around each of the {args.steps} timed thins'
+                          + (' (max over ranks)' if sharded else ''),
+                'flop_per_pair': flop_per_pair, 'fp64_instr_per_pair': instr_per_pair,
+                'fp64_issue': {'achieved_Tinstr_s': round(gins, 2), 'peak_Tinstr_s': round(issue_peak, 2),
+                               'frac': round(gins / issue_peak, 4)},
+                'note': ('compute-bound: the persistent kernel keeps the rows in VGPR/AGPR/LDS across the m steps '
+                         '(PMC traffic per launch = "traffic", far below the streaming figure), so the roofline is '
+                         'fp64 VALU (MI355X fp64 vector peak 78.6 TF = fp64 matrix peak; no MFMA shape fits '
+                         'the per-pair scalar work); one wave per SIMD issues fp64 at ~7-12 cycles '
+                         '(profiles/r01_fp64_rate.log), ~30% of each step is the in-launch exchange'),
+                'hbm_view': {'algorithmic_bytes_per_launch': alg_bytes, 'bytes_per_pair': bytes_per_pair,
+                             'achieved_GBs': round(alg_bytes / avg / 1e9, 1), 'peak_GBs': HBM_PEAK_GBS,
+                             'frac': round(alg_bytes / avg / 1e9 / HBM_PEAK_GBS, 4)},
+            }
+        if not sharded and not args.no_kernel_timing:
+            s_avg, s_med = kernel_timing(prob, min(m, 200))
+            step = {
+                'kernel': f'greedy_step_ct<{d}> (launch-per-step path, st_greedy_steps)' if d <= 8 else
+                          'greedy_step_rt (launch-per-step path, st_greedy_steps)',
+                'avg_us': round(s_avg * 1e6, 2), 'median_us': round(s_med * 1e6, 2),
+                'achieved_GBs': round(n * bytes_per_pair / s_avg / 1e9, 1),
+                'frac_hbm': round(n * bytes_per_pair / s_avg / 1e9 / HBM_PEAK_GBS, 4),
+                'algorithmic_bytes_per_launch': n * bytes_per_pair}
+            if persistent:
+                roofline['step_kernel'] = step
+            else:
+                rec = pmc_rec.get(args.config)
+                roofline = {'bound': 'hbm', 'achieved': step['achieved_GBs'], 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                            'frac': step['frac_hbm'], 'traffic': round(rec['hbm_bytes_per_launch']) if rec else None,
+                            'kernel': step['kernel'], 'kernel_avg_us': step['avg_us'],
+                            'kernel_median_us': step['median_us'],
+                            'algorithmic_bytes_per_launch': step['algorithmic_bytes_per_launch'],
+                            'bytes_per_pair': bytes_per_pair,
+                            'timing': 'HIP events around back-to-back single-step launches'}
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg, integrand, args.cpu_steps)
 

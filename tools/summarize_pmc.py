@@ -38,6 +38,8 @@ def main():
     kname, fetch_kib, nf = pick(f, 'FETCH_SIZE')
     _, write_kib, nw = pick(w, 'WRITE_SIZE')
     rec = {'kernel': kname, 'launches_fetch': nf, 'launches_write': nw,
+           'note': ('8-B-per-lane loads (dwordx2) are outside the guide\'s calibration; the same 128-B-request '
+                    'x2 correction is applied') if 'persistent' in kname else '',
            'FETCH_SIZE_KiB_per_launch': fetch_kib, 'WRITE_SIZE_KiB_per_launch': write_kib,
            'read_bytes_per_launch': 2 * fetch_kib * 1024, 'write_bytes_per_launch': write_kib * 1024,
            'hbm_bytes_per_launch': (2 * fetch_kib + write_kib) * 1024,
