@@ -253,7 +253,7 @@ __global__ __launch_bounds__(kBlock) void greedy_step_ct(GreedyArgs a) {
 // Runtime-d variant (any 1 <= d <= 128): one candidate per lane per iteration, selected row in LDS.
 // ------------------------------------------------------------------------------------------
 template <bool GF, bool DIAG>
-__global__ __launch_bounds__(kBlock) void greedy_step_rt(GreedyArgs a) {
+__global__ __launch_bounds__(kBlock, 4) void greedy_step_rt(GreedyArgs a) {
     __shared__ double s_row[2 * kMaxDim + 1];
     __shared__ double s_v[kWaves];
     __shared__ int64_t s_i[kWaves];
@@ -278,9 +278,12 @@ __global__ __launch_bounds__(kBlock) void greedy_step_rt(GreedyArgs a) {
             if constexpr (GF) kv = (kv * a.w[i]) * a.w[i];
             a.A[i] = kv;
         } else {
-            kv = pair_value_rt(a.x + i, a.g + i, ld, s_row, s_row + d, 1, d, l, l2, tr);
-            if constexpr (GF) kv = (kv * a.w[i]) * wj;
-            kv = a.A[i] + 2.0 * kv;
+            const double ai = a.A[i];
+            const double wi = GF ? a.w[i] : 1.0;
+            kv = d >= 8 ? pair_value_rt8(a.x + i, a.g + i, ld, s_row, s_row + d, d, l, l2, tr)
+                        : pair_value_rt(a.x + i, a.g + i, ld, s_row, s_row + d, 1, d, l, l2, tr);
+            if constexpr (GF) kv = (kv * wi) * wj;
+            kv = ai + 2.0 * kv;
             a.A[i] = kv;
         }
         if (better(kv, i, best_v, best_i)) { best_v = kv; best_i = i; }
@@ -338,10 +341,12 @@ __global__ __launch_bounds__(kBlock) void greedy_finalize(const double* __restri
 static int g_max_blocks = 256;
 static int g_cpt = -1;
 static int g_pf = -1;
+static int g_rt_max_blocks = kMaxBlocks;
 constexpr int64_t kLargeShard = 1000000;
 
 int tune(int key, int value) {
     switch (key) {
+        case 6: if (value < 1 || value > kMaxBlocks) return -1; g_rt_max_blocks = value; return 0;
         case 0: if (value < 1 || value > kMaxBlocks) return -1; g_max_blocks = value; return 0;
         case 1: if (value != -1 && value != 1 && value != 2 && value != 4) return -1; g_cpt = value; return 0;
         case 2: if (value < -1 || value > 1) return -1; g_pf = value; return 0;
@@ -366,7 +371,10 @@ int greedy_blocks(int64_t n, int d) {
     variant_for(n, d, cpt, pf);
     const int64_t per_block = (int64_t)cpt * kBlock;
     int64_t b = (n + per_block - 1) / per_block;
-    if (b > g_max_blocks) b = g_max_blocks;
+    // d > 8: one candidate per lane and a long dependent chain per candidate -- latency is hidden
+    // by waves, not by registers: up to 4 blocks (16 waves) per CU
+    const int cap = d > kMaxCtDim ? g_rt_max_blocks : g_max_blocks;
+    if (b > cap) b = cap;
     if (b < 1) b = 1;
     return (int)b;
 }

@@ -234,6 +234,53 @@ __device__ __forceinline__ double pair_value_rt(const double* __restrict__ xa,
     return finish_pair(qs, t1s, t2s, t3s, tr);
 }
 
+// Runtime d >= 8 (the high-dimensional streaming step): the candidate's coordinates are loaded
+// eight at a time (16 independent loads in flight per lane; 4 waves per SIMD hide the rest),
+// matching NumPy's pairwise_sum lane structure for t3 (r[k % 8]).
+// The selected point (xb, gb) is block-uniform (LDS broadcast reads).  Same bits as pair_value_rt.
+__device__ __forceinline__ double pair_value_rt8(const double* __restrict__ xa,
+                                                const double* __restrict__ ga, int64_t sa,
+                                                const double* xb, const double* gb, int d,
+                                                double l, double l2, double tr) {
+    double qs = 0.0, t1s = 0.0, t2s = 0.0;
+    double r[8];
+    const int full = d - (d % 8);
+    for (int k0 = 0; k0 < full; k0 += 8) {
+        double cx[8], cg[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) { cx[j] = xa[(k0 + j) * sa]; cg[j] = ga[(k0 + j) * sa]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = k0 + j;
+            const double xbk = xb[k], gbk = gb[k];
+            const double dl = cx[j] - xbk;
+            const double gd = cg[j] - gbk;
+            const double q = (l * dl) * dl;
+            const double u = (l2 * dl) * dl;
+            const double v = (l * gd) * dl;
+            if (k0 == 0 && j == 0) {
+                qs = q; t1s = u; t2s = v;
+            } else {
+                qs = qs + q; t1s = t1s + u; t2s = t2s + v;
+            }
+            const double p = cg[j] * gbk;
+            r[j] = k0 == 0 ? p : r[j] + p;
+        }
+    }
+    double t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (int k = full; k < d; ++k) {
+        const double xak = xa[k * sa], gak = ga[k * sa];
+        const double xbk = xb[k], gbk = gb[k];
+        const double dl = xak - xbk;
+        const double gd = gak - gbk;
+        qs = qs + (l * dl) * dl;
+        t1s = t1s + (l2 * dl) * dl;
+        t2s = t2s + (l * gd) * dl;
+        t3s += gak * gbk;
+    }
+    return finish_pair(qs, t1s, t2s, t3s, tr);
+}
+
 __device__ __forceinline__ double diag_value_rt(const double* __restrict__ gi_col, int64_t ld,
                                                 int d, double tr) {
     double r[8];
