@@ -183,7 +183,13 @@ def main():
     ap.add_argument('--no-kernel-timing', action='store_true')
     ap.add_argument('--no-graph', action='store_true', help='N > 1: eager per-step launches instead of a HIP graph')
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
+    ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
+    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd'],
+                    help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
+                         '(row-sharded, RCCL all-reduce of the n-length column-sum vector)')
     args = ap.parse_args()
+    if args.workload == 'ksd':
+        return main_ksd(args)
 
     import torch
     import torch.distributed as dist
@@ -362,6 +368,96 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if sharded:
+        dist.destroy_process_group()
+
+
+def main_ksd(args):
+    """Full-sample cumulative KSD of the config's sample (stein_thinning.stein.ksd over all n rows):
+    n(n-1)/2 off-diagonal pair-evaluations per step.  N > 1: the triangle's rows are split into
+    pair-balanced blocks, every rank sums its rows into the n-length column-sum vector, one RCCL
+    all-reduce, every rank finishes the prefix scan (stein_thinning/distributed.py run_ksd_sharded)."""
+    import torch
+    import torch.distributed as dist
+    from stein_thinning import distributed as sd
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = int(os.environ.get('LOCAL_RANK', 0))
+    torch.cuda.set_device(local)
+    dev = torch.device('cuda', local)
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        os.environ.setdefault('MASTER_PORT', '29531')
+        dist.init_process_group('nccl', device_id=dev)
+    cfg = CONFIGS[args.config if args.config != 'c4' or args.ksd_full else 'c2']
+    integrand, _, _ = make_integrand(cfg)
+    n, d = cfg['n'], integrand.sample.shape[1]
+    be = sd.HipKsdBackend(integrand, n)
+    a0, a1 = sd.triangle_row_bounds(n, rank, world)
+    ks = torch.empty(n, dtype=torch.float64, device=dev)
+    from stein_thinning import _native as nat
+    L = nat.lib()
+    p = be.prob
+    stream = torch.cuda.current_stream()
+
+    def run_once():
+        c = be.colsum(a0, a1)
+        if world > 1:
+            dist.all_reduce(c)
+        nat.check(L.st_ksd_finish(nat.ptr(p.x), nat.ptr(p.g), nat.ptr(p.w), n, p.ld, p.d, p.l, p.tr,
+                                  nat.ptr(c), nat.ptr(ks), nat.stream_handle()), 'st_ksd_finish')
+    for _ in range(args.warmup):
+        run_once()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ce = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    e0.record(stream)
+    for c0, c1 in ce:
+        c0.record(stream)
+        be.colsum(a0, a1)
+        c1.record(stream)
+    e1.record(stream)
+    torch.cuda.synchronize()
+    colsum_s = float(np.mean([c0.elapsed_time(c1) * 1e-3 for c0, c1 in ce]))
+    # full steps (column sums + all-reduce + finish)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run_once()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed, colsum_s], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed, colsum_s = (float(v) for v in tt.tolist())
+    gf = integrand.weights is not None
+    pairs = n * (n - 1) / 2
+    rank_pairs = sum(n - 1 - a for a in range(a0, a1)) if n < 10 ** 4 else \
+        (a1 - a0) * (n - 1) - (a1 * (a1 - 1) - a0 * (a0 - 1)) // 2
+    flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0) + 1     # + the column accumulate
+    if rank == 0:
+        tflops = rank_pairs * flop_per_pair / colsum_s / 1e12
+        line = {
+            'metric': 'Stein-kernel pair-evals/s, full-sample cumulative KSD (stein.ksd over all n rows)',
+            'value': pairs * args.steps / elapsed, 'unit': 'pair-evals/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': elapsed / args.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'strong', 'vs_baseline': None, 'dtype': 'f64',
+            'data': 'synthetic (seeded RW-MH LV-surrogate chains; see bench.py docstring)',
+            'config': {'workload': f"full-sample KSD of config {cfg['desc']}", 'n': n, 'd': d,
+                       'kernel': 'gradient-free' if gf else 'langevin',
+                       'parallelism': f'triangle rows x{world}, RCCL all-reduce of the n-vector' if world > 1
+                       else 'single-gpu'},
+            'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
+                         'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': None,
+                         'kernel': f'ksd_colsum_kernel<{d},{str(gf).lower()}>', 'kernel_avg_us': round(colsum_s * 1e6, 1),
+                         'flop_per_pair': flop_per_pair},
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 

@@ -313,8 +313,7 @@ int st_kernel_pairs(const double* x_soa, const double* g_soa, const double* weig
 
 int64_t st_ksd_workspace_bytes(int64_t m, int64_t ld) {
     if (m < 1 || ld < m) return -1;
-    const int64_t ntiles = (m + 63) / 64;
-    return ntiles * ld * 8;
+    return ld * 8;   // the column-sum vector
 }
 
 int st_ksd_cumulative(const double* x_soa, const double* g_soa, const double* weights, int64_t m,
@@ -326,13 +325,36 @@ int st_ksd_cumulative(const double* x_soa, const double* g_soa, const double* we
     if (workspace_bytes < st_ksd_workspace_bytes(m, ld))
         return fail(ST_ERR_INVALID, "workspace too small");
     hipStream_t s = static_cast<hipStream_t>(stream);
-    const int64_t ntiles = (m + 63) / 64;
-    if (ntiles > 65535) return fail(ST_ERR_UNSUPPORTED, "m too large for the tiled KSD grid");
     st::PairArgs p{x_soa, g_soa, weights, ld, d, linv_scale, linv_trace};
-    double* part = static_cast<double*>(workspace);
-    rc = hip_check(st::launch_ksd_rows(p, nullptr, m, part, ntiles, s), "ksd rows launch");
+    double* csum = static_cast<double*>(workspace);
+    rc = hip_check(st::launch_ksd_colsum(p, m, 0, m, csum, s), "ksd column-sum launch");
     if (rc) return rc;
-    return hip_check(st::launch_ksd_scan(part, m, ld, ks_out, s), "ksd scan launch");
+    return hip_check(st::launch_ksd_finish(p, m, csum, ks_out, s), "ksd finish launch");
+}
+
+int st_ksd_colsum(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
+                  int64_t ld, int32_t d, double linv_scale, double linv_trace, int64_t row_begin,
+                  int64_t row_end, double* csum_out, void* stream) {
+    int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
+    if (rc) return rc;
+    if (!csum_out) return fail(ST_ERR_INVALID, "NULL output");
+    if (row_begin < 0 || row_end < row_begin || row_end > n)
+        return fail(ST_ERR_INVALID, "need 0 <= row_begin <= row_end <= n");
+    st::PairArgs p{x_soa, g_soa, weights, ld, d, linv_scale, linv_trace};
+    return hip_check(st::launch_ksd_colsum(p, n, row_begin, row_end, csum_out,
+                                           static_cast<hipStream_t>(stream)),
+                     "ksd column-sum launch");
+}
+
+int st_ksd_finish(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
+                  int64_t ld, int32_t d, double linv_scale, double linv_trace, const double* csum,
+                  double* ks_out, void* stream) {
+    int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
+    if (rc) return rc;
+    if (!csum || !ks_out) return fail(ST_ERR_INVALID, "NULL pointer");
+    st::PairArgs p{x_soa, g_soa, weights, ld, d, linv_scale, linv_trace};
+    return hip_check(st::launch_ksd_finish(p, n, csum, ks_out, static_cast<hipStream_t>(stream)),
+                     "ksd finish launch");
 }
 
 int st_kmat(const double* x_soa, const double* g_soa, const double* weights, int64_t k, int64_t ld,

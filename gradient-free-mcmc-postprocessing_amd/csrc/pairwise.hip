@@ -3,13 +3,14 @@
 // * pairs:     out[p] = k(i1[p], i2[p]) -- the integrand protocol integrand(ind1, ind2) of the
 //              reference (stein_thinning.thinning._make_stein_integrand / _make_stein_gf_integrand;
 //              used at code/src/utils/ksd.py:9-16, JAX_Stein_Thinning.ipynb cells 17, 30).
-// * ksd rows:  LDS-tiled lower triangle of the selected set's Gram matrix: per (row tile, column
-//              tile) partial row sums r_i = 2 sum_{j<i} k_ij + k_ii (stein_thinning.stein.ksd,
-//              called at code/src/utils/ksd.py:27; report.tex:311-313).
-// * ksd scan:  ps_i = sum_{a<=i} r_a, ks_i = sqrt(ps_i) / (i+1).
+// * ksd:       column sums of the strictly lower triangle (K6, below; stein_thinning.stein.ksd,
+//              called at code/src/utils/ksd.py:27; report.tex:311-313), then
+//              ps_i = sum_{a<=i} (2 csum_a + k_aa), ks_i = sqrt(ps_i) / (i+1).
 // * kmat:      K[r, c] = integrand(min(r,c), max(r,c)) (stein_thinning.stein.kmat,
 //              code/tests/test_ksd.py:20, Gaussian_mixture.ipynb cell 94).
 // All operate on a compact SoA problem (leading dimension ld); fp64 VALU bound, no MFMA.
+#include <type_traits>
+
 #include "stein_math.hpp"
 #include "stein_internal.hpp"
 
@@ -49,76 +50,6 @@ __device__ __forceinline__ void stage_chunk(const PairArgs& p, int64_t m, int64_
     }
 }
 
-// KSD: grid (ntiles_j, ntiles_i); block 256 = 4 waves; lane <-> row i; wave w takes columns
-// w, w+4, ... of each staged chunk.  part[bj * ld + i] = this tile's share of r_i.
-__global__ __launch_bounds__(256) void ksd_rows_kernel(PairArgs p, int64_t m,
-                                                       double* __restrict__ part) {
-    const int64_t bi = blockIdx.y, bj = blockIdx.x;
-    if (bj > bi) return;
-    __shared__ double s[2 * kMaxDim + 1][kChunk];
-    __shared__ double s_red[4][kTile];
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int64_t i = bi * kTile + lane;
-    const double l2 = p.l * p.l;
-    const int d = p.d;
-    const double wi = (p.w && i < m) ? p.w[i] : 1.0;
-    double acc = 0.0;
-    const int64_t cend = (bj * kTile + kTile < m) ? bj * kTile + kTile : m;
-    for (int64_t c0 = bj * kTile; c0 < cend; c0 += kChunk) {
-        __syncthreads();
-        stage_chunk(p, m, c0, s);
-        __syncthreads();
-        if (i < m) {
-            for (int c = wave; c < kChunk; c += 4) {
-                const int64_t j = c0 + c;
-                if (j > i || j >= m) continue;
-                double kv = pair_value_rt(p.x + i, p.g + i, p.ld, &s[0][c], &s[d][c], kChunk, d,
-                                          p.l, l2, p.tr);
-                if (p.w) kv = (kv * wi) * s[2 * d][c];
-                acc += (j < i) ? 2.0 * kv : kv;
-            }
-        }
-    }
-    s_red[wave][lane] = acc;
-    __syncthreads();
-    if (wave == 0 && i < m)
-        part[bj * p.ld + i] = ((s_red[0][lane] + s_red[1][lane]) + s_red[2][lane]) + s_red[3][lane];
-}
-
-// r_i = sum over column tiles bj <= bi of part; then a single-block prefix sum -> ks.
-__global__ __launch_bounds__(1024) void ksd_scan_kernel(const double* __restrict__ part,
-                                                        int64_t ld, int64_t m,
-                                                        double* __restrict__ ks) {
-    __shared__ double s_tot[1024];
-    const int tid = threadIdx.x;
-    const int64_t per = (m + blockDim.x - 1) / blockDim.x;
-    const int64_t b = tid * per, e = (b + per < m) ? b + per : m;
-    double run = 0.0;
-    for (int64_t i = b; i < e; ++i) {
-        const int64_t bi = i / kTile;
-        double r = 0.0;
-        for (int64_t bj = 0; bj <= bi; ++bj) r += part[bj * ld + i];
-        run += r;
-        ks[i] = r;  // temporarily hold r_i
-    }
-    s_tot[tid] = run;
-    __syncthreads();
-    if (tid == 0) {
-        double acc = 0.0;
-        for (int t = 0; t < (int)blockDim.x; ++t) {
-            const double v = s_tot[t];
-            s_tot[t] = acc;
-            acc += v;
-        }
-    }
-    __syncthreads();
-    double ps = s_tot[tid];
-    for (int64_t i = b; i < e; ++i) {
-        ps += ks[i];
-        ks[i] = __builtin_sqrt(ps) / (double)(i + 1);
-    }
-}
-
 // kmat: grid (ntiles, ntiles); lane <-> row r of the tile, columns staged; out is (k, k) row-major
 // and symmetric by construction (weights applied in (min, max) order), so the lane-contiguous
 // store out[c * k + r] is coalesced.
@@ -151,6 +82,204 @@ __global__ __launch_bounds__(256) void kmat_kernel(PairArgs p, int64_t k, double
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// K6 -- full-sample KSD at scale: column sums of the strictly lower triangle over a row range
+//   csum[i] = sum_{a in [a0, a1), a < i} k(x_i, x_a)   ((k w_i) w_a for gradient-free),
+// i.e. the reference's 2*np.sum(k0[:i]) term of stein_thinning.stein.ksd (restated in
+// oracle/stein_numpy.py ksd; report.tex:311-313) split over row ranges.  A row-sharded multi-GPU
+// run computes csum over its rows and all-reduces the n-length vector (RCCL) before ksd_finish.
+// One thread per column i (its row in registers); rows a staged kRows at a time in LDS and read
+// as block-uniform broadcasts; 4 blocks (16 waves) per CU; block b takes column block NB-1-b so
+// the heavy (late) columns are dispatched first.  Per pair: the bits of pair_value_ct (the
+// range-guarded fast arithmetic when the block's columns and the staged rows admit it); per
+// column: a sequential sum in increasing a.
+// ------------------------------------------------------------------------------------------
+constexpr int kColBlock = 256;
+
+struct ColsumArgs {
+    const double* x;
+    const double* g;
+    const double* w;
+    int64_t n, ld;
+    double l, tr;
+    int64_t a0, a1;
+    double* csum;
+};
+
+template <int D, bool GF>
+__global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) {
+    constexpr int R = kColBlock;
+    __shared__ double sx[D][R];
+    __shared__ double sg[D][R];
+    __shared__ double sw[GF ? R : 1];
+    const int tid = threadIdx.x;
+    const int64_t nb = (p.n + R - 1) / R;
+    const int64_t c0 = (nb - 1 - (int64_t)blockIdx.x) * R;
+    const int64_t i = c0 + tid;
+    const int64_t ld = p.ld;
+    double xi[D], gi[D];
+    const bool live = i < p.n;
+    int cok = fast_range_ok(p.l) & (int)(p.l > 0.0) & (int)(p.tr > 0.0) & (int)(p.tr <= 0x1p64);
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        xi[k] = live ? p.x[k * ld + i] : 0.0;
+        gi[k] = live ? p.g[k * ld + i] : 0.0;
+        cok &= fast_range_ok(xi[k]) & fast_range_ok(gi[k]);
+    }
+    const double wi = (GF && live) ? p.w[i] : 1.0;
+    const double l = p.l, l2 = p.l * p.l, tr = p.tr;
+    const int col_fast = __syncthreads_and(cok);
+    const int64_t a_stop = p.a1 < c0 + R ? p.a1 : c0 + R;   // rows a < i <= c0 + R - 1
+    double acc = 0.0;
+    for (int64_t ac = p.a0; ac < a_stop; ac += R) {
+        const int64_t a = ac + tid;
+        int rok = 1;
+        __syncthreads();
+        if (a < a_stop) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const double xv = p.x[k * ld + a], gv = p.g[k * ld + a];
+                sx[k][tid] = xv;
+                sg[k][tid] = gv;
+                rok &= fast_range_ok(xv) & fast_range_ok(gv);
+            }
+            if constexpr (GF) sw[tid] = p.w[a];
+        }
+        const int fast = __syncthreads_and(rok) & col_fast;
+        const int cnt = (int)((a_stop - ac) < R ? (a_stop - ac) : R);
+        auto sweep = [&](auto fast_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value;
+            asm volatile(";; colsum variant" ::);
+            for (int e = 0; e < cnt; ++e) {
+                double xa[D], ga[D];
+#pragma unroll
+                for (int k = 0; k < D; ++k) { xa[k] = sx[k][e]; ga[k] = sg[k][e]; }
+                double kv = pair_value_ct<D, FAST>(xi, gi, xa, ga, l, l2, tr);
+                if constexpr (GF) kv = (kv * wi) * sw[e];
+                acc = (ac + e < i) ? acc + kv : acc;
+            }
+        };
+        if (fast) sweep(std::true_type{});
+        else sweep(std::false_type{});
+    }
+    if (live) p.csum[i] = acc;
+}
+
+// d > 8: the column's coordinates are re-read (L1/L2) per pair; rows staged kRowsRt at a time.
+constexpr int kRowsRt = 32;
+template <bool GF>
+__global__ __launch_bounds__(kColBlock) void ksd_colsum_rt_kernel(ColsumArgs p, int d) {
+    __shared__ double srow[2 * kMaxDim][kRowsRt];
+    __shared__ double sw[kRowsRt];
+    const int tid = threadIdx.x;
+    const int64_t nb = (p.n + kColBlock - 1) / kColBlock;
+    const int64_t c0 = (nb - 1 - (int64_t)blockIdx.x) * kColBlock;
+    const int64_t i = c0 + tid;
+    const int64_t ld = p.ld;
+    const bool live = i < p.n;
+    const int64_t ic = live ? i : 0;
+    const double wi = (GF && live) ? p.w[i] : 1.0;
+    const double l = p.l, l2 = p.l * p.l, tr = p.tr;
+    const int64_t a_stop = p.a1 < c0 + kColBlock ? p.a1 : c0 + kColBlock;
+    double acc = 0.0;
+    for (int64_t ac = p.a0; ac < a_stop; ac += kRowsRt) {
+        const int cnt = (int)((a_stop - ac) < kRowsRt ? (a_stop - ac) : kRowsRt);
+        __syncthreads();
+        for (int e = tid; e < 2 * d * kRowsRt; e += kColBlock) {
+            const int k = e / kRowsRt, r = e % kRowsRt;
+            if (r < cnt) srow[k][r] = k < d ? p.x[(int64_t)k * ld + ac + r] : p.g[(int64_t)(k - d) * ld + ac + r];
+        }
+        if (GF && tid < cnt) sw[tid] = p.w[ac + tid];
+        __syncthreads();
+        for (int e = 0; e < cnt; ++e) {
+            double kv = pair_value_rt(p.x + ic, p.g + ic, ld, &srow[0][e], &srow[d][e], kRowsRt, d,
+                                      l, l2, tr);
+            if constexpr (GF) kv = (kv * wi) * sw[e];
+            acc = (ac + e < i) ? acc + kv : acc;
+        }
+    }
+    if (live) p.csum[i] = acc;
+}
+
+// ks_i = sqrt(S_i) / (i+1), S_i = sum_{a <= i} (2 csum_a + k(a, a)); single block: contiguous
+// chunk per thread, exclusive scan of the 1024 chunk totals, second pass writes ks.
+__global__ __launch_bounds__(1024) void ksd_finish_kernel(ColsumArgs p, int d, double* __restrict__ ks) {
+    __shared__ double s_tot[1024];
+    const int tid = threadIdx.x;
+    const int64_t m = p.n;
+    const int64_t per = (m + blockDim.x - 1) / blockDim.x;
+    const int64_t b = tid * per, e = (b + per < m) ? b + per : m;
+    double run = 0.0;
+    for (int64_t i = b; i < e; ++i) {
+        double kd = diag_value_rt(p.g + i, p.ld, d, p.tr);
+        if (p.w) kd = (kd * p.w[i]) * p.w[i];
+        const double r = 2.0 * p.csum[i] + kd;
+        run += r;
+        ks[i] = r;
+    }
+    s_tot[tid] = run;
+    __syncthreads();
+    if (tid == 0) {
+        double acc = 0.0;
+        for (int t = 0; t < (int)blockDim.x; ++t) {
+            const double v = s_tot[t];
+            s_tot[t] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    double ps = s_tot[tid];
+    for (int64_t i = b; i < e; ++i) {
+        ps += ks[i];
+        ks[i] = __builtin_sqrt(ps) / (double)(i + 1);
+    }
+}
+
+template <int D>
+static void launch_colsum_ct(const ColsumArgs& a, unsigned grid, hipStream_t s) {
+    if (a.w) ksd_colsum_kernel<D, true><<<grid, kColBlock, 0, s>>>(a);
+    else ksd_colsum_kernel<D, false><<<grid, kColBlock, 0, s>>>(a);
+}
+
+hipError_t launch_ksd_colsum(const PairArgs& p, int64_t n, int64_t a0, int64_t a1, double* csum,
+                             hipStream_t s) {
+    ColsumArgs a{p.x, p.g, p.w, n, p.ld, p.l, p.tr, a0, a1, csum};
+    // columns at or below a0 get no rows: zero them, then launch only the blocks above a0
+    const int64_t first_block = (a0 + 1) / kColBlock;          // block containing column a0 + 1
+    const int64_t nb = (n + kColBlock - 1) / kColBlock;
+    if (first_block * kColBlock > 0) {
+        hipError_t e = hipMemsetAsync(csum, 0, (size_t)(first_block * kColBlock < n ? first_block * kColBlock : n) * 8, s);
+        if (e != hipSuccess) return e;
+    }
+    if (nb <= first_block || a1 <= a0) {
+        if (nb > first_block) return hipMemsetAsync(csum, 0, (size_t)n * 8, s);
+        return hipSuccess;
+    }
+    const unsigned grid = (unsigned)(nb - first_block);   // block b -> column block nb-1-b
+    switch (p.d) {
+        case 1: launch_colsum_ct<1>(a, grid, s); break;
+        case 2: launch_colsum_ct<2>(a, grid, s); break;
+        case 3: launch_colsum_ct<3>(a, grid, s); break;
+        case 4: launch_colsum_ct<4>(a, grid, s); break;
+        case 5: launch_colsum_ct<5>(a, grid, s); break;
+        case 6: launch_colsum_ct<6>(a, grid, s); break;
+        case 7: launch_colsum_ct<7>(a, grid, s); break;
+        case 8: launch_colsum_ct<8>(a, grid, s); break;
+        default:
+            if (a.w) ksd_colsum_rt_kernel<true><<<grid, kColBlock, 0, s>>>(a, p.d);
+            else ksd_colsum_rt_kernel<false><<<grid, kColBlock, 0, s>>>(a, p.d);
+            break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t launch_ksd_finish(const PairArgs& p, int64_t n, const double* csum, double* ks,
+                             hipStream_t s) {
+    ColsumArgs a{p.x, p.g, p.w, n, p.ld, p.l, p.tr, 0, 0, const_cast<double*>(csum)};
+    ksd_finish_kernel<<<1, 1024, 0, s>>>(a, p.d, ks);
+    return hipGetLastError();
+}
+
 __global__ void layout_soa_kernel(const double* __restrict__ rowmajor, int64_t n, int d, int64_t ld,
                                   double* __restrict__ soa) {
     const int64_t total = n * d;
@@ -172,19 +301,6 @@ static int grid_for(int64_t work, int block) {
 hipError_t launch_pairs(const PairArgs& p, const int64_t* i1, const int64_t* i2, int64_t L,
                         double* out, hipStream_t s) {
     pairs_kernel<<<grid_for(L, 256), 256, 0, s>>>(p, i1, i2, L, out);
-    return hipGetLastError();
-}
-
-hipError_t launch_ksd_rows(const PairArgs& p, const int64_t* idx, int64_t m, double* part,
-                           int64_t ntiles, hipStream_t s) {
-    (void)idx;
-    dim3 grid((unsigned)ntiles, (unsigned)ntiles);
-    ksd_rows_kernel<<<grid, 256, 0, s>>>(p, m, part);
-    return hipGetLastError();
-}
-
-hipError_t launch_ksd_scan(const double* part, int64_t m, int64_t ld, double* ks, hipStream_t s) {
-    ksd_scan_kernel<<<1, 1024, 0, s>>>(part, ld, m, ks);
     return hipGetLastError();
 }
 

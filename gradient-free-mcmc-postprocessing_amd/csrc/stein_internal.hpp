@@ -79,12 +79,12 @@ struct PairArgs {
 
 hipError_t launch_pairs(const PairArgs& p, const int64_t* i1, const int64_t* i2, int64_t L,
                         double* out, hipStream_t s);
-hipError_t launch_ksd_rows(const PairArgs& p, const int64_t* idx, int64_t m, double* part,
-                           int64_t ntiles, hipStream_t s);
-hipError_t launch_ksd_scan(const double* part, int64_t m, int64_t ld, double* ks,
-                           hipStream_t s);
 hipError_t launch_kmat(const PairArgs& p, const int64_t* idx, int64_t k, double* out,
                        hipStream_t s);
+hipError_t launch_ksd_colsum(const PairArgs& p, int64_t n, int64_t a0, int64_t a1, double* csum,
+                             hipStream_t s);
+hipError_t launch_ksd_finish(const PairArgs& p, int64_t n, const double* csum, double* ks,
+                             hipStream_t s);
 hipError_t launch_layout_soa(const double* rowmajor, int64_t n, int d, int64_t ld, double* soa,
                              hipStream_t s);
 

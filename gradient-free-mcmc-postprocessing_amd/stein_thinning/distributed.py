@@ -319,6 +319,91 @@ class PersistentShardedGreedy:
         return self.indices()
 
 
+# --------------------------------------------------------------------------------------------
+# Full-sample KSD, row-sharded: every rank sums k(i, a) over its rows a < i for all columns i,
+# the n-length column-sum vector is all-reduced (RCCL), every rank finishes the prefix scan.
+# --------------------------------------------------------------------------------------------
+def triangle_row_bounds(n: int, rank: int, world: int):
+    """Row block [a0, a1) of rank such that the strictly-lower-triangle pair counts
+    sum_{a in [a0, a1)} (n - 1 - a) are balanced across ranks."""
+    total = n * (n - 1) // 2
+
+    def first_row(target):   # smallest a0 with pairs(rows < a0) >= target
+        if target <= 0:
+            return 0
+        # pairs(rows < a) = a (n - 1) - a (a - 1) / 2, increasing in a on [0, n]
+        lo, hi = 0, n
+        while lo < hi:
+            mid = (lo + hi) // 2
+            if mid * (n - 1) - mid * (mid - 1) // 2 >= target:
+                hi = mid
+            else:
+                lo = mid + 1
+        return lo
+    a0 = first_row(total * rank // world) if rank > 0 else 0
+    a1 = first_row(total * (rank + 1) // world) if rank + 1 < world else n
+    return a0, a1
+
+
+class HipKsdBackend:
+    """Device side of the sharded KSD: the full problem resident on this rank's GPU."""
+
+    def __init__(self, integrand: SteinIntegrand, n: int):
+        import torch
+        self.prob = integrand.device_problem()
+        self.n = int(n)
+        if not 0 <= self.n <= self.prob.n:
+            raise ValueError(f'n = {n} outside [0, {self.prob.n}]')
+        self.csum = torch.zeros(max(self.prob.ld, 1), dtype=torch.float64, device=self.prob.device)
+
+    def colsum(self, a0: int, a1: int):
+        p = self.prob
+        nat.check(nat.lib().st_ksd_colsum(nat.ptr(p.x), nat.ptr(p.g), nat.ptr(p.w), self.n, p.ld, p.d,
+                                          p.l, p.tr, a0, a1, nat.ptr(self.csum), nat.stream_handle()),
+                  'st_ksd_colsum')
+        return self.csum[:self.n]
+
+    def finish(self, csum) -> np.ndarray:
+        import torch
+        p = self.prob
+        ks = torch.empty(self.n, dtype=torch.float64, device=p.device)
+        nat.check(nat.lib().st_ksd_finish(nat.ptr(p.x), nat.ptr(p.g), nat.ptr(p.w), self.n, p.ld, p.d,
+                                          p.l, p.tr, nat.ptr(csum), nat.ptr(ks), nat.stream_handle()),
+                  'st_ksd_finish')
+        return ks.cpu().numpy()
+
+
+def _all_reduce_sum(t, group=None) -> None:
+    """In-place sum over ranks: RCCL on the device buffer (nccl), host round trip under gloo."""
+    import torch.distributed as dist
+    if t.is_cuda and dist.get_backend(group) != 'nccl':
+        h = t.cpu()
+        dist.all_reduce(h, group=group)
+        t.copy_(h)
+    else:
+        dist.all_reduce(t, group=group)
+
+
+def run_ksd_sharded(backend, n: int, group=None) -> np.ndarray:
+    """Drive colsum over this rank's triangle rows -> all-reduce of the n-vector -> finish.
+    ``backend`` exposes colsum(a0, a1) -> tensor and finish(tensor) -> ndarray (HipKsdBackend;
+    tests substitute a CPU backend)."""
+    rank, world = _world(group)
+    if n == 0:
+        return np.empty(0)
+    a0, a1 = triangle_row_bounds(n, rank, world)
+    c = backend.colsum(a0, a1)
+    if world > 1:
+        _all_reduce_sum(c, group)
+    return backend.finish(c)
+
+
+def ksd_sharded(integrand: SteinIntegrand, n: int, group=None) -> np.ndarray:
+    """Cumulative KSD of rows 0..n-1 of ``integrand`` (stein_thinning.stein.ksd semantics) with
+    the O(n^2) pair work split over the ranks of ``group``."""
+    return run_ksd_sharded(HipKsdBackend(integrand, n), int(n), group)
+
+
 def _world(group):
     import torch.distributed as dist
     if not dist.is_available() or not dist.is_initialized():

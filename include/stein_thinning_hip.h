@@ -159,10 +159,26 @@ int st_kernel_pairs(const double *x_soa, const double *g_soa, const double *weig
  * ks_out[i] = sqrt(sum_{a,b <= i} k(a,b)) / (i+1).  kmat_out is the full symmetric (k, k)
  * row-major matrix K[r][c] = k(min(r,c), max(r,c)).
  * ---------------------------------------------------------------------------------------- */
-int64_t st_ksd_workspace_bytes(int64_t m, int64_t ld);
+int64_t st_ksd_workspace_bytes(int64_t m, int64_t ld);   /* ld doubles: the column-sum vector */
 int st_ksd_cumulative(const double *x_soa, const double *g_soa, const double *weights, int64_t m,
                       int64_t ld, int32_t d, double linv_scale, double linv_trace, double *ks_out,
                       void *workspace, int64_t workspace_bytes, void *stream);
+/*
+ * Full-sample KSD at scale, row-sharded across GPUs (the n-length column-sum all-reduce):
+ *   st_ksd_colsum:  csum_out[i] = sum_{a in [row_begin, row_end), a < i} k(i, a)   (i < n)
+ *                   -- the 2*np.sum(k0[:i]) / 2 term of the reference's ksd loop restricted to a
+ *                   row range; ranks cover disjoint row ranges and all-reduce (sum) csum;
+ *   st_ksd_finish:  ks_out[i] = sqrt(sum_{a <= i} (2 csum[a] + k(a, a))) / (i + 1).
+ * st_ksd_cumulative == st_ksd_colsum over [0, m) followed by st_ksd_finish.
+ * Summation order differs from the reference's NumPy pairwise sums (floating-point tolerance).
+ */
+int st_ksd_colsum(const double *x_soa, const double *g_soa, const double *weights, int64_t n,
+                  int64_t ld, int32_t d, double linv_scale, double linv_trace, int64_t row_begin,
+                  int64_t row_end, double *csum_out, void *stream);
+int st_ksd_finish(const double *x_soa, const double *g_soa, const double *weights, int64_t n,
+                  int64_t ld, int32_t d, double linv_scale, double linv_trace, const double *csum,
+                  double *ks_out, void *stream);
+
 int st_kmat(const double *x_soa, const double *g_soa, const double *weights, int64_t k,
             int64_t ld, int32_t d, double linv_scale, double linv_trace, double *kmat_out,
             void *stream);

@@ -80,3 +80,34 @@ class CpuShardBackend:
 
     def indices(self):
         return self.idx.copy()
+
+
+class CpuKsdBackend:
+    """CPU stand-in for HipKsdBackend: column sums of the lower triangle over a row range with the
+    C bit model's pair values (same per-column sequential order as the HIP kernel)."""
+
+    def __init__(self, s, gs, w, l, tr, n):
+        self.s, self.gs, self.w, self.l, self.tr, self.n = s[:n], gs[:n], w, l, tr, n
+
+    def colsum(self, a0, a1):
+        c = np.zeros(self.n)
+        for i in range(a0 + 1, self.n):
+            a = np.arange(a0, min(i, a1))
+            if a.size == 0:
+                continue
+            kv = oracle_c.pairs(self.s, self.gs, None, self.l, self.tr, np.full(a.size, i), a)
+            if self.w is not None:
+                kv = (kv * self.w[i]) * self.w[a]
+            acc = 0.0
+            for v in kv:
+                acc += v
+            c[i] = acc
+        return torch.from_numpy(c)
+
+    def finish(self, c):
+        ar = np.arange(self.n)
+        kd = oracle_c.pairs(self.s, self.gs, None, self.l, self.tr, ar, ar)
+        if self.w is not None:
+            kd = (kd * self.w[:self.n]) * self.w[:self.n]
+        S = np.cumsum(2.0 * c.numpy() + kd)
+        return np.sqrt(S) / (ar + 1)

@@ -11,7 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import stein_numpy as o
-from stein_thinning.distributed import run_sharded, shard_bounds
+from stein_thinning.distributed import run_ksd_sharded, run_sharded, shard_bounds, triangle_row_bounds
 
 
 def _free_port():
@@ -71,3 +71,43 @@ def test_shard_bounds_cover_rows():
             assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
             sizes = [e - s for s, e in b]
             assert max(sizes) - min(sizes) <= 1
+
+
+def _ksd_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from tests.cpu_shard_backend import CpuKsdBackend
+        x, g, log_p, log_q = _data(True)
+        s, gs = o._validate_and_standardize(x, g, True)
+        w = np.exp(o._log_weights(log_p, log_q, None))
+        linv = o.make_precon(s, 'med')
+        n = 400
+        ks = run_ksd_sharded(CpuKsdBackend(s, gs, w, linv[0, 0], np.trace(linv), n), n)
+        np.save(os.path.join(out_dir, f'ks{rank}.npy'), ks)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world', [2, 3])
+def test_ksd_row_sharded_all_reduce(tmp_path, world):
+    """Row-sharded KSD: triangle row blocks + gloo all-reduce of the column-sum vector reproduce
+    the reference's cumulative KSD (oracle ksd over the gradient-free integrand)."""
+    mp.spawn(_ksd_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    x, g, log_p, log_q = _data(True)
+    want = o.ksd(o._make_stein_gf_integrand(x, log_p, log_q, g, preconditioner='med'), 400)
+    for r in range(world):
+        np.testing.assert_allclose(np.load(tmp_path / f'ks{r}.npy'), want, rtol=1e-12)
+
+
+def test_triangle_row_bounds_balance():
+    for n in [1, 2, 5, 1000, 2_000_000]:
+        for world in [1, 2, 3, 8]:
+            b = [triangle_row_bounds(n, r, world) for r in range(world)]
+            assert b[0][0] == 0 and b[-1][1] == n
+            assert all(b[i][1] == b[i + 1][0] for i in range(world - 1))
+            pairs = [sum(n - 1 - a for a in range(a0, a1)) if n < 5000 else
+                     (a1 - a0) * (n - 1) - (a1 * (a1 - 1) - a0 * (a0 - 1)) // 2 for a0, a1 in b]
+            assert sum(pairs) == n * (n - 1) // 2
+            if n >= 1000:
+                assert max(pairs) - min(pairs) <= 2 * n
