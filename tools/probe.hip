@@ -102,7 +102,9 @@ int main(int argc, char** argv) {
     const double bytes_rw = (double)n * (16 * d + 16), bytes_r = (double)n * (16 * d + 8);
     printf("# n=%lld d=%d  step traffic %.1f MB (read %.1f MB)\n", (long long)n, d, bytes_rw / 1e6, bytes_r / 1e6);
     const int reps = 200;
+    const bool persist_only = argc > 2 && argv[2][0] == 'p';
     for (int blocks : {256, 512, 1024, 2048, 4096}) {
+        if (persist_only) break;
         for (int wr = 0; wr < 2; ++wr) {
             for (int cpt : {2, 4}) {
                 auto launch = [&]() {
@@ -133,6 +135,7 @@ int main(int argc, char** argv) {
     const double l = 0.37, tr = 4 * 0.37;
     const int M = reps + 1;
     for (int blocks : {128, 256, 512, 1024}) {
+        if (persist_only) break;
         for (int cpt : {1, 2, 4}) {
             for (int pf = 0; pf < 2; ++pf) {
                 st_tune(0, blocks);
