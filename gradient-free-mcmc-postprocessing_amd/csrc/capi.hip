@@ -357,6 +357,25 @@ int st_ksd_finish(const double* x_soa, const double* g_soa, const double* weight
                      "ksd finish launch");
 }
 
+int st_distance_colsum(const double* a_soa, int64_t lda, int64_t na, const double* b_soa,
+                       int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
+                       int32_t triangle, double* out, void* stream) {
+    if (na == 0) return ST_OK;
+    if (!a_soa || !b_soa || !out) return fail(ST_ERR_INVALID, "NULL pointer");
+    if (d < 1 || d > st::kMaxDim) return fail(ST_ERR_UNSUPPORTED, "unsupported d = %d", d);
+    if (na < 0 || nb < 0 || lda < na || ldb < nb || (lda & 7) || (ldb & 7))
+        return fail(ST_ERR_INVALID, "bad sizes (ld must be a multiple of 8 and >= the row count)");
+    if (b_begin < 0 || b_end < b_begin || b_end > nb)
+        return fail(ST_ERR_INVALID, "need 0 <= b_begin <= b_end <= nb");
+    if (triangle && (a_soa != b_soa || lda != ldb))
+        return fail(ST_ERR_INVALID, "triangle=1 needs A and B to be the same array");
+    if ((na + 255) / 256 > 0x7FFFFFFFll) return fail(ST_ERR_UNSUPPORTED, "na too large");
+    return hip_check(st::launch_distance_colsum(a_soa, lda, na, b_soa, ldb, b_begin, b_end, d,
+                                                triangle ? 1 : 0, out,
+                                                static_cast<hipStream_t>(stream)),
+                     "distance column-sum launch");
+}
+
 int st_kmat(const double* x_soa, const double* g_soa, const double* weights, int64_t k, int64_t ld,
             int32_t d, double linv_scale, double linv_trace, double* kmat_out, void* stream) {
     int rc = check_problem(x_soa, g_soa, weights, k, d, ld);

@@ -235,6 +235,113 @@ __global__ __launch_bounds__(1024) void ksd_finish_kernel(ColsumArgs p, int d, d
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// K7 -- energy distance (dcor.energy_distance, used by the reference's fit_quality,
+// Comparison.ipynb cell 19 / Gradient_free_Student_t.ipynb; Gaussian_mixture.ipynb cells 63-71):
+//   out[i] = sum_{b in [b0, b1), (!tri or b < i)} || A_i - B_b ||_2
+// Euclidean distance as scipy's cdist: sqrt of the sequential sum over k of (a_k - b_k)^2.
+// Same structure as K6: one A point per thread, B points staged in LDS, block-uniform reads.
+// ------------------------------------------------------------------------------------------
+struct DistArgs {
+    const double* a;
+    int64_t lda, na;
+    const double* b;
+    int64_t ldb;
+    int64_t b0, b1;
+    int tri;
+    double* out;
+};
+
+template <int D>
+__global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
+    constexpr int R = kColBlock;
+    __shared__ double sb[D][R];
+    const int tid = threadIdx.x;
+    const int64_t nb = (p.na + R - 1) / R;
+    const int64_t c0 = (nb - 1 - (int64_t)blockIdx.x) * R;
+    const int64_t i = c0 + tid;
+    const bool live = i < p.na;
+    double ai[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) ai[k] = live ? p.a[k * p.lda + i] : 0.0;
+    int64_t b_stop = p.b1;
+    if (p.tri && c0 + R < b_stop) b_stop = c0 + R;
+    double acc = 0.0;
+    for (int64_t bc = p.b0; bc < b_stop; bc += R) {
+        __syncthreads();
+        const int64_t bb = bc + tid;
+        if (bb < b_stop) {
+#pragma unroll
+            for (int k = 0; k < D; ++k) sb[k][tid] = p.b[k * p.ldb + bb];
+        }
+        __syncthreads();
+        const int cnt = (int)((b_stop - bc) < R ? (b_stop - bc) : R);
+        for (int e = 0; e < cnt; ++e) {
+            double ss = 0.0;
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const double dk = ai[k] - sb[k][e];
+                ss += dk * dk;
+            }
+            const double dist = __builtin_sqrt(ss);
+            acc = (!p.tri || bc + e < i) ? acc + dist : acc;
+        }
+    }
+    if (live) p.out[i] = acc;
+}
+
+__global__ __launch_bounds__(kColBlock) void dist_colsum_rt_kernel(DistArgs p, int d) {
+    constexpr int R = kRowsRt;
+    __shared__ double sb[kMaxDim][R];
+    const int tid = threadIdx.x;
+    const int64_t nb = (p.na + kColBlock - 1) / kColBlock;
+    const int64_t c0 = (nb - 1 - (int64_t)blockIdx.x) * kColBlock;
+    const int64_t i = c0 + tid;
+    const bool live = i < p.na;
+    const int64_t ic = live ? i : 0;
+    int64_t b_stop = p.b1;
+    if (p.tri && c0 + kColBlock < b_stop) b_stop = c0 + kColBlock;
+    double acc = 0.0;
+    for (int64_t bc = p.b0; bc < b_stop; bc += R) {
+        const int cnt = (int)((b_stop - bc) < R ? (b_stop - bc) : R);
+        __syncthreads();
+        for (int e = tid; e < d * R; e += kColBlock) {
+            const int k = e / R, r = e % R;
+            if (r < cnt) sb[k][r] = p.b[(int64_t)k * p.ldb + bc + r];
+        }
+        __syncthreads();
+        for (int e = 0; e < cnt; ++e) {
+            double ss = 0.0;
+            for (int k = 0; k < d; ++k) {
+                const double dk = p.a[(int64_t)k * p.lda + ic] - sb[k][e];
+                ss += dk * dk;
+            }
+            const double dist = __builtin_sqrt(ss);
+            acc = (!p.tri || bc + e < i) ? acc + dist : acc;
+        }
+    }
+    if (live) p.out[i] = acc;
+}
+
+hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, const double* b,
+                                  int64_t ldb, int64_t b0, int64_t b1, int d, int tri,
+                                  double* out, hipStream_t s) {
+    DistArgs p{a, lda, na, b, ldb, b0, b1, tri, out};
+    const unsigned grid = (unsigned)((na + kColBlock - 1) / kColBlock);
+    switch (d) {
+        case 1: dist_colsum_kernel<1><<<grid, kColBlock, 0, s>>>(p); break;
+        case 2: dist_colsum_kernel<2><<<grid, kColBlock, 0, s>>>(p); break;
+        case 3: dist_colsum_kernel<3><<<grid, kColBlock, 0, s>>>(p); break;
+        case 4: dist_colsum_kernel<4><<<grid, kColBlock, 0, s>>>(p); break;
+        case 5: dist_colsum_kernel<5><<<grid, kColBlock, 0, s>>>(p); break;
+        case 6: dist_colsum_kernel<6><<<grid, kColBlock, 0, s>>>(p); break;
+        case 7: dist_colsum_kernel<7><<<grid, kColBlock, 0, s>>>(p); break;
+        case 8: dist_colsum_kernel<8><<<grid, kColBlock, 0, s>>>(p); break;
+        default: dist_colsum_rt_kernel<<<grid, kColBlock, 0, s>>>(p, d); break;
+    }
+    return hipGetLastError();
+}
+
 template <int D>
 static void launch_colsum_ct(const ColsumArgs& a, unsigned grid, hipStream_t s) {
     if (a.w) ksd_colsum_kernel<D, true><<<grid, kColBlock, 0, s>>>(a);

@@ -55,6 +55,8 @@ SIGNATURES = {
                                      _c_dp, _c_dp]),
     'st_ksd_finish': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i64, _i32, _f64, _f64, _c_dp,
                                      _c_dp, _c_dp]),
+    'st_distance_colsum': (ctypes.c_int, [_c_dp, _i64, _i64, _c_dp, _i64, _i64, _i32, _i64, _i64,
+                                          _i32, _c_dp, _c_dp]),
     'st_mailbox_bytes': (_i64, [_i32]),
     'st_mailbox_alloc': (ctypes.c_int, [_i64, ctypes.POINTER(ctypes.c_void_p)]),
     'st_mailbox_free': (ctypes.c_int, [_c_dp]),

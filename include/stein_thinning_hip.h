@@ -183,6 +183,18 @@ int st_kmat(const double *x_soa, const double *g_soa, const double *weights, int
             int64_t ld, int32_t d, double linv_scale, double linv_trace, double *kmat_out,
             void *stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Energy distance -- replaces dcor.energy_distance(x, y) (V-statistic, exponent 1) as used by the
+ * reference's fit_quality (code/notebooks/lotka_volterra/Comparison.ipynb cell 19,
+ * Gradient_free_Student_t.ipynb; Gaussian_mixture.ipynb cells 63-71):
+ *   out[i] = sum_{b in [b_begin, b_end), (!triangle or b < i)} ||A_i - B_b||_2,   i < na
+ * A, B SoA (d, lda) / (d, ldb); triangle = 1 requires B == A (strict lower triangle: self sums).
+ * ED(x, y) = 2 sum(out(x; y)) / (nx ny) - 2 sum(out(x; x, tri)) / nx^2 - 2 sum(out(y; y, tri)) / ny^2.
+ * ---------------------------------------------------------------------------------------- */
+int st_distance_colsum(const double *a_soa, int64_t lda, int64_t na, const double *b_soa,
+                       int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
+                       int32_t triangle, double *out, void *stream);
+
 /* row-major (n, d) -> SoA (d, ld) layout helper (device to device) */
 int st_layout_soa(const double *rowmajor, int64_t n, int32_t d, int64_t ld, double *soa,
                   void *stream);
