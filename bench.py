@@ -208,7 +208,7 @@ def main():
 
     cfg = CONFIGS[args.config]
     n, m = cfg['n'], cfg['m']
-    integrand, _, _ = make_integrand(cfg)
+    integrand, host_x, host_g = make_integrand(cfg)
     d = integrand.sample.shape[1]
 
     if not sharded:
@@ -341,6 +341,17 @@ def main():
                             'timing': 'HIP events around back-to-back single-step launches'}
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg, integrand, args.cpu_steps)
+        e2e = None
+        if world == 1 and not cfg['gf'] and not cfg.get('d50'):
+            # the drop-in call on host arrays (not `value`): standardisation + 'med' + H2D upload +
+            # SoA layout + the persistent launch + D2H of the indices
+            from stein_thinning import thinning as st
+            st.thin(host_x, host_g, m, preconditioner='med')
+            t_e = time.perf_counter()
+            e2e_idx = st.thin(host_x, host_g, m, preconditioner='med')
+            e2e = {'thin_host_arrays_s': round(time.perf_counter() - t_e, 4),
+                   'pair_evals_per_s': n * m / (time.perf_counter() - t_e),
+                   'same_indices': bool(np.array_equal(e2e_idx, result_idx))}
 
     if rank == 0:
         pairs = float(n) * m * args.steps
@@ -365,6 +376,7 @@ def main():
                        'first_indices': result_idx[:8].tolist()},
             'roofline': roofline,
             'cpu_baseline': cpu,
+            'end_to_end': e2e if rank == 0 and not sharded else None,
         }
         print(json.dumps(line), flush=True)
     if sharded:

@@ -57,6 +57,8 @@ SIGNATURES = {
                                      _c_dp, _c_dp]),
     'st_distance_colsum': (ctypes.c_int, [_c_dp, _i64, _i64, _c_dp, _i64, _i64, _i32, _i64, _i64,
                                           _i32, _c_dp, _c_dp]),
+    'st_standardize_host': (ctypes.c_int, [_c_dp, _c_dp, _i64, _i32, _i32, _c_dp, _c_dp, _c_dp, _c_dp,
+                                           ctypes.POINTER(ctypes.c_int32)]),
     'st_mailbox_bytes': (_i64, [_i32]),
     'st_mailbox_alloc': (ctypes.c_int, [_i64, ctypes.POINTER(ctypes.c_void_p)]),
     'st_mailbox_free': (ctypes.c_int, [_c_dp]),
@@ -100,6 +102,11 @@ def lib() -> ctypes.CDLL:
                 import torch  # noqa: F401  -- map torch's HIP runtime before ours resolves against it
                 _LIB = load_library()
     return _LIB
+
+
+def check_host(rc: int, what: str = '') -> None:
+    if rc != ST_OK:
+        raise ValueError(f'{what}: invalid arguments ({rc})')
 
 
 def check(rc: int, what: str = '') -> None:

@@ -37,7 +37,7 @@ def _as_numpy(a) -> np.ndarray:
     return np.asarray(a, dtype=np.float64)
 
 
-def _validate_sample_and_gradient(sample: np.ndarray, gradient: np.ndarray) -> None:
+def _validate_shapes(sample: np.ndarray, gradient: np.ndarray) -> None:
     if sample.ndim != 2 or gradient.ndim != 2:
         raise ValueError('sample or gradient is not two-dimensional.')
     n, d = sample.shape
@@ -45,29 +45,38 @@ def _validate_sample_and_gradient(sample: np.ndarray, gradient: np.ndarray) -> N
         raise ValueError('sample is empty.')
     if gradient.shape != (n, d):
         raise ValueError('Dimensions of sample and gradient are inconsistent.')
-    if np.isnan(sample).any() or np.isnan(gradient).any():
-        raise ValueError('sample or gradient contains NaNs.')
-    if np.isinf(sample).any() or np.isinf(gradient).any():
-        raise ValueError('sample or gradient contains infs.')
 
 
 def _validate_and_standardize(sample, gradient, standardize: bool = True):
     """Validate, then (optionally) scale each dimension by its mean absolute deviation.
 
     loc = mean(x, 0); scl = mean(|x - loc|, 0); x / scl, g * scl  (per-dimension scaling pinned
-    by the golden indices of ``Gradient_free_Stein_thinning.ipynb`` cell 8).
+    by the golden indices of ``Gradient_free_Stein_thinning.ipynb`` cell 8).  Evaluated by the
+    host routine ``st_standardize_host`` of the native library in three passes (the NumPy
+    expressions' reduction orders reproduced bit for bit; tests/test_shim_host.py), errors as the
+    NumPy checks raise them.
     """
-    sample = _as_numpy(sample)
-    gradient = _as_numpy(gradient)
-    _validate_sample_and_gradient(sample, gradient)
-    if standardize:
-        loc = np.mean(sample, axis=0)
-        scl = np.mean(np.abs(sample - loc), axis=0)
-        if np.min(scl) == 0:
-            raise ValueError('Too few unique samples in smp.')
-        sample = sample / scl
-        gradient = gradient * scl
-    return sample, gradient
+    import ctypes
+    from . import _native as nat
+    sample = np.ascontiguousarray(_as_numpy(sample))
+    gradient = np.ascontiguousarray(_as_numpy(gradient))
+    _validate_shapes(sample, gradient)
+    n, d = sample.shape
+    if d == 1 and np.getbufsize() != 8192:     # the native column sum models the default bufsize
+        return _validate_and_standardize_numpy(sample, gradient, standardize)
+    out_s = np.empty_like(sample) if standardize else sample
+    out_g = np.empty_like(gradient) if standardize else gradient
+    status = ctypes.c_int32(0)
+    nat.check_host(nat.lib().st_standardize_host(
+        sample.ctypes.data, gradient.ctypes.data, n, d, 1 if standardize else 0, out_s.ctypes.data,
+        out_g.ctypes.data, None, None, ctypes.byref(status)), 'st_standardize_host')
+    if status.value == 1:
+        raise ValueError('sample or gradient contains NaNs.')
+    if status.value == 2:
+        raise ValueError('sample or gradient contains infs.')
+    if status.value == 3:
+        raise ValueError('Too few unique samples in smp.')
+    return out_s, out_g
 
 
 def _log_weights(log_p: np.ndarray, log_q: np.ndarray, range_cap: Optional[float]) -> np.ndarray:
@@ -85,6 +94,23 @@ def _log_weights(log_p: np.ndarray, log_q: np.ndarray, range_cap: Optional[float
     if range_cap is not None:
         log_ratio = np.minimum(log_ratio, range_cap)
     return log_ratio
+
+
+def _validate_and_standardize_numpy(sample, gradient, standardize):
+    """The NumPy expressions themselves (host preprocessing; used only when NumPy's ufunc buffer
+    size was changed from its default, which the native routine models)."""
+    if np.isnan(sample).any() or np.isnan(gradient).any():
+        raise ValueError('sample or gradient contains NaNs.')
+    if np.isinf(sample).any() or np.isinf(gradient).any():
+        raise ValueError('sample or gradient contains infs.')
+    if standardize:
+        loc = np.mean(sample, axis=0)
+        scl = np.mean(np.abs(sample - loc), axis=0)
+        if np.min(scl) == 0:
+            raise ValueError('Too few unique samples in smp.')
+        sample = sample / scl
+        gradient = gradient * scl
+    return sample, gradient
 
 
 class SteinIntegrand:

@@ -195,6 +195,17 @@ int st_distance_colsum(const double *a_soa, int64_t lda, int64_t na, const doubl
                        int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
                        int32_t triangle, double *out, void *stream);
 
+/* ------------------------------------------------------------------------------------------
+ * Host-side input preparation -- stein_thinning.thinning._validate_and_standardize (restated at
+ * JAX_Stein_Thinning.ipynb cells 15-18): NaN / inf checks, then per-dimension
+ * loc = mean(x, 0), scl = mean(|x - loc|, 0), x / scl, g * scl, bit-identical to the NumPy
+ * expressions (their reduction orders reproduced).  Row-major (n, d) host arrays; outputs may
+ * alias the inputs.  *status: 0 ok, 1 NaN, 2 inf, 3 a zero scale.  No HIP calls.
+ * ---------------------------------------------------------------------------------------- */
+int st_standardize_host(const double *sample, const double *gradient, int64_t n, int32_t d,
+                        int32_t standardize, double *sample_out, double *gradient_out,
+                        double *loc_out, double *scl_out, int32_t *status);
+
 /* row-major (n, d) -> SoA (d, ld) layout helper (device to device) */
 int st_layout_soa(const double *rowmajor, int64_t n, int32_t d, int64_t ld, double *soa,
                   void *stream);

@@ -141,3 +141,56 @@ def test_import_touches_no_gpu():
     import os
     subprocess.run([sys.executable, '-c', code], check=True,
                    cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def _numpy_standardize(sample, gradient):
+    """The reference's NumPy expressions (oracle restatement, JAX_Stein_Thinning.ipynb cells 15-18)."""
+    loc = np.mean(sample, axis=0)
+    scl = np.mean(np.abs(sample - loc), axis=0)
+    return sample / scl, gradient * scl
+
+
+@pytest.mark.parametrize('n,d', [(1, 3), (7, 1), (9, 1), (129, 1), (1000, 1), (250_003, 1), (1000, 2),
+                                 (100_001, 4), (3000, 50), (20, 128)])
+def test_native_standardize_bitwise_numpy(n, d):
+    """st_standardize_host (native, three passes) == the NumPy expressions bit for bit, for the
+    row-wise (d >= 2) and the pairwise (d == 1) reduction orders."""
+    rng = np.random.default_rng(n + d)
+    x = rng.normal(size=(n, d)) * rng.uniform(1e-3, 1e3, size=d) + rng.normal(size=d) * 10
+    if n > 1:
+        x[n // 2] = x[0]
+    g = rng.normal(size=(n, d))
+    if n == 1:
+        with pytest.raises(ValueError, match='Too few unique samples'):
+            st._validate_and_standardize(x, g)
+        return
+    xs, gs = st._validate_and_standardize(x, g)
+    wx, wg = _numpy_standardize(x, g)
+    assert xs.dtype == np.float64 and xs.shape == (n, d)
+    np.testing.assert_array_equal(xs.view(np.uint64), wx.view(np.uint64))
+    np.testing.assert_array_equal(gs.view(np.uint64), wg.view(np.uint64))
+    # inputs untouched, standardize=False returns the validated inputs
+    xs2, gs2 = st._validate_and_standardize(x, g, standardize=False)
+    np.testing.assert_array_equal(xs2, x)
+    np.testing.assert_array_equal(gs2, g)
+
+
+def test_native_standardize_errors_and_inputs():
+    x = np.arange(12.0).reshape(6, 2)
+    g = np.ones((6, 2))
+    for bad, msg in [((np.nan, 0), 'NaNs'), ((np.inf, 0), 'infs')]:
+        xb = x.copy()
+        xb[2, 1] = bad[0]
+        with pytest.raises(ValueError, match=msg):
+            st._validate_and_standardize(xb, g)
+        with pytest.raises(ValueError, match=msg):
+            st._validate_and_standardize(x, np.where(xb != xb, np.nan, np.where(np.isinf(xb), np.inf, g)))
+    xc = x.copy()
+    xc[:, 1] = 3.0
+    with pytest.raises(ValueError, match='Too few unique samples'):
+        st._validate_and_standardize(xc, g)
+    # Fortran-ordered / float32 / list inputs are converted like np.asarray(dtype=float64)
+    xs, gs = st._validate_and_standardize(np.asfortranarray(x), g.astype(np.float32))
+    wx, wg = _numpy_standardize(x, g)
+    np.testing.assert_array_equal(xs, wx)
+    np.testing.assert_array_equal(gs, wg)
