@@ -13,6 +13,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <initializer_list>
+
 #include <algorithm>
 #include <thread>
 #include <vector>
@@ -69,15 +71,29 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
         return ST_ERR_INVALID;
     *status = 0;
     const int64_t total = n * (int64_t)d;
+    const int hw = hardware_threads();
+    // run fn(t, T) on T threads (T = 1: inline)
+    auto parallel = [](int T, auto&& fn) {
+        if (T <= 1) { fn(0, 1); return; }
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) th.emplace_back([&fn, t, T] { fn(t, T); });
+        for (auto& x : th) x.join();
+    };
     // pass 1: NaN / inf flags (NaN reported first, as the NumPy checks run in that order)
-    bool nan = false, inf = false;
-    for (int64_t e = 0; e < total; ++e) {
-        const double xv = sample[e], gv = gradient[e];
-        nan |= (xv != xv) | (gv != gv);
-        inf |= (fabs(xv) == INFINITY) | (fabs(gv) == INFINITY);
-    }
-    if (nan) { *status = 1; return ST_OK; }
-    if (inf) { *status = 2; return ST_OK; }
+    const int tn = (int)std::max<int64_t>(1, std::min<int64_t>(hw, total / (1 << 18)));
+    std::vector<int> nanf(tn, 0), inff(tn, 0);
+    parallel(tn, [&](int t, int T) {
+        bool nan = false, inf = false;
+        for (int64_t e = total * t / T; e < total * (t + 1) / T; ++e) {
+            const double xv = sample[e], gv = gradient[e];
+            nan |= (xv != xv) | (gv != gv);
+            inf |= (fabs(xv) == INFINITY) | (fabs(gv) == INFINITY);
+        }
+        nanf[t] = nan;
+        inff[t] = inf;
+    });
+    for (int t = 0; t < tn; ++t) if (nanf[t]) { *status = 1; return ST_OK; }
+    for (int t = 0; t < tn; ++t) if (inff[t]) { *status = 2; return ST_OK; }
     if (!standardize) {
         if (sample_out != sample) memcpy(sample_out, sample, (size_t)total * 8);
         if (gradient_out != gradient) memcpy(gradient_out, gradient, (size_t)total * 8);
@@ -91,40 +107,37 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
         for (int64_t i = 0; i < n; ++i) dev[i] = fabs(sample[i] - loc[0]);
         scl[0] = numpy_column_sum(dev.data(), n) / dn;
     } else {
-        // row-by-row accumulation: acc[j] += x[i, j] (NumPy's axis-0 reduction order)
-        std::vector<double> acc(sample, sample + d);
-        for (int64_t i = 1; i < n; ++i) {
-            const double* row = sample + i * d;
-            for (int j = 0; j < d; ++j) acc[j] += row[j];
-        }
-        for (int j = 0; j < d; ++j) loc[j] = acc[j] / dn;
-        for (int j = 0; j < d; ++j) acc[j] = fabs(sample[j] - loc[j]);
-        for (int64_t i = 1; i < n; ++i) {
-            const double* row = sample + i * d;
-            for (int j = 0; j < d; ++j) acc[j] += fabs(row[j] - loc[j]);
-        }
-        for (int j = 0; j < d; ++j) scl[j] = acc[j] / dn;
+        // row-by-row accumulation acc[j] += x[i, j] (NumPy's axis-0 reduction order): sequential
+        // per column, so the columns are split over threads (contiguous column groups)
+        const int tc = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)hw, (int64_t)d, n / 65536}));
+        parallel(tc, [&](int t, int T) {
+            const int j0 = d * t / T, j1 = d * (t + 1) / T, w = j1 - j0;
+            std::vector<double> acc(sample + j0, sample + j1);
+            for (int64_t i = 1; i < n; ++i) {
+                const double* row = sample + i * d + j0;
+                for (int j = 0; j < w; ++j) acc[j] += row[j];
+            }
+            for (int j = 0; j < w; ++j) loc[j0 + j] = acc[j] / dn;
+            for (int j = 0; j < w; ++j) acc[j] = fabs(sample[j0 + j] - loc[j0 + j]);
+            for (int64_t i = 1; i < n; ++i) {
+                const double* row = sample + i * d + j0;
+                for (int j = 0; j < w; ++j) acc[j] += fabs(row[j] - loc[j0 + j]);
+            }
+            for (int j = 0; j < w; ++j) scl[j0 + j] = acc[j] / dn;
+        });
     }
     for (int j = 0; j < d; ++j)
         if (scl[j] == 0.0) { *status = 3; return ST_OK; }
     if (loc_out) memcpy(loc_out, loc.data(), (size_t)d * 8);
     if (scl_out) memcpy(scl_out, scl.data(), (size_t)d * 8);
     // pass 3: x / scl, g * scl -- elementwise, row blocks in parallel
-    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(hardware_threads(), n / 65536));
-    auto scale = [&](int64_t r0, int64_t r1) {
-        for (int64_t i = r0; i < r1; ++i)
+    const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(hw, n / 65536));
+    parallel(nt, [&](int t, int T) {
+        for (int64_t i = n * t / T; i < n * (t + 1) / T; ++i)
             for (int j = 0; j < d; ++j) {
                 sample_out[i * d + j] = sample[i * d + j] / scl[j];
                 gradient_out[i * d + j] = gradient[i * d + j] * scl[j];
             }
-    };
-    if (nt == 1) {
-        scale(0, n);
-    } else {
-        std::vector<std::thread> th;
-        for (int t = 0; t < nt; ++t)
-            th.emplace_back(scale, n * t / nt, n * (t + 1) / nt);
-        for (auto& x : th) x.join();
-    }
+    });
     return ST_OK;
 }

@@ -37,6 +37,20 @@ def _as_numpy(a) -> np.ndarray:
     return np.asarray(a, dtype=np.float64)
 
 
+def _host_buffer(shape) -> np.ndarray:
+    """float64 host array for standardised data that is about to be uploaded: page-locked memory
+    from torch's caching host allocator when a HIP device is present (the upload then runs at
+    PCIe DMA speed instead of registering fresh pageable pages: 1 ms vs ~6 ms per 64 MB on the
+    MI355X box), plain NumPy memory otherwise."""
+    try:
+        import torch
+        if torch.cuda.is_available():
+            return torch.empty(shape, dtype=torch.float64, pin_memory=True).numpy()
+    except Exception:   # noqa: BLE001 -- pinned memory is an optimisation only
+        pass
+    return np.empty(shape, dtype=np.float64)
+
+
 def _validate_shapes(sample: np.ndarray, gradient: np.ndarray) -> None:
     if sample.ndim != 2 or gradient.ndim != 2:
         raise ValueError('sample or gradient is not two-dimensional.')
@@ -64,8 +78,8 @@ def _validate_and_standardize(sample, gradient, standardize: bool = True):
     n, d = sample.shape
     if d == 1 and np.getbufsize() != 8192:     # the native column sum models the default bufsize
         return _validate_and_standardize_numpy(sample, gradient, standardize)
-    out_s = np.empty_like(sample) if standardize else sample
-    out_g = np.empty_like(gradient) if standardize else gradient
+    out_s = _host_buffer(sample.shape) if standardize else sample
+    out_g = _host_buffer(gradient.shape) if standardize else gradient
     status = ctypes.c_int32(0)
     nat.check_host(nat.lib().st_standardize_host(
         sample.ctypes.data, gradient.ctypes.data, n, d, 1 if standardize else 0, out_s.ctypes.data,
