@@ -198,13 +198,25 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             if constexpr (GF) rowv[2 * D] = a.w[r];
         };
         int ok_all = 1;
-        for (unsigned it = 0;; ++it) {
+        unsigned it = 0;
+        // one 16-B sc1 buffer load per record (both granules; a torn pair fails its tag check)
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bank), 0,
+                                                            G * kRecGranules * 8, 0x00020000);
+        typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+        for (;; ++it) {
+            // all four loads unconditionally (records past G read as zeros: the descriptor's range
+            // check), so they issue back to back and a poll costs ONE round trip, not four
+            u32x4 qs[kMaxGrid / 64];
+#pragma unroll
+            for (int c = 0; c < kMaxGrid / 64; ++c)
+                qs[c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (lane + 64 * c) * kRecGranules * 8,
+                                                              0, 16 /* sc1 */);
 #pragma unroll
             for (int c = 0; c < kMaxGrid / 64; ++c) {
                 if ((need & ~seen) & (1u << c)) {
-                    const uint64_t* gr = bank + (int64_t)(lane + 64 * c) * kRecGranules;
-                    const uint64_t g0 = __hip_atomic_load(gr + 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    const uint64_t g1 = __hip_atomic_load(gr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    const u32x4 q = qs[c];
+                    const uint64_t g0 = ((uint64_t)q.y << 32) | q.x;
+                    const uint64_t g1 = ((uint64_t)q.w << 32) | q.z;
                     if (((g0 & 0xFF00000000000000ull) == want) & ((g1 & 0xFF00000000000000ull) == want)) {
                         seen |= 1u << c;
                         const double rv = __longlong_as_double(
@@ -229,6 +241,10 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             }
         }
         ST_STAMP(a, t + 1, 1);
+#ifdef ST_PERSIST_STAMPS
+        if (a.stamps && lane == 0 && t + 1 >= kStampFirst && t + 1 < kStampFirst + kStampSteps)
+            a.stamps[((int64_t)blockIdx.x * kStampSteps + (t + 1 - kStampFirst)) * kStampPhases + 9] = it + 1;
+#endif
         int64_t my = gi;
         p_wave_minloc(v, gi);
         ST_STAMP(a, t + 1, 7);

@@ -240,6 +240,15 @@ int main(int argc, char** argv) {
                     mloc += (double)(q[7] - q[1]);
                     if (q[8]) { tot += 1; late += q[8] == 2; }
                 }
+            double its = 0, swt = 0;
+            for (int st = 1; st < SP; ++st)
+                for (int b = 0; b < G; ++b) {
+                    const uint64_t* q = &h[((size_t)b * SP + st) * PH];
+                    its += (double)q[9];
+                    swt += (double)(q[1] - q[0]);
+                }
+            printf("sweep: %.2f polls per step on average, %.3f us per poll\n", its / ((SP - 1) * G),
+                   swt / its / 100);
             printf("sweep-done -> minloc-done %.2f us; winner row loaded after the sweep in %.0f%% of steps\n",
                    mloc / ((SP - 1) * G) / 100, tot > 0 ? 100.0 * late / tot : -1.0);
         }
