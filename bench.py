@@ -172,6 +172,43 @@ def kernel_timing(prob, n_points: int, repeats: int = 5):
     return float(np.mean(per)), float(np.median(per))
 
 
+# Rehearsal mode (ST_BENCH_SHARE_DEVICE=1, never used by the driver): every rank on cuda:0 and a
+# gloo group, so the N > 1 flow (mailbox setup, device exchange, timing reductions) can run on a
+# one-GPU box with several processes sharing the device.
+SHARE_DEVICE = os.environ.get('ST_BENCH_SHARE_DEVICE') == '1'
+
+
+def _setup_ranks():
+    import torch
+    rank = int(os.environ.get('RANK', 0))
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    local = 0 if SHARE_DEVICE else int(os.environ.get('LOCAL_RANK', 0))
+    torch.cuda.set_device(local)
+    return rank, world, torch.device('cuda', local)
+
+
+def _init_group(dev):
+    import torch.distributed as dist
+    os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+    os.environ.setdefault('MASTER_PORT', '29531')
+    os.environ.setdefault('RANK', os.environ.get('RANK', '0'))
+    os.environ.setdefault('WORLD_SIZE', os.environ.get('WORLD_SIZE', '1'))
+    if SHARE_DEVICE:
+        dist.init_process_group('gloo')
+    else:
+        dist.init_process_group('nccl', device_id=dev)
+
+
+def _max_over_ranks(values, dev):
+    """Element-wise max over ranks of a list of floats (RCCL, or gloo on host tensors)."""
+    import torch
+    import torch.distributed as dist
+    on = dev if dist.get_backend() == 'nccl' else torch.device('cpu')
+    t = torch.tensor(values, dtype=torch.float64, device=on)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return [float(v) for v in t.tolist()]
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
@@ -193,18 +230,13 @@ def main():
 
     import torch
     import torch.distributed as dist
-    rank = int(os.environ.get('RANK', 0))
-    world = int(os.environ.get('WORLD_SIZE', 1))
-    local = int(os.environ.get('LOCAL_RANK', 0))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    rank, world, dev = _setup_ranks()
     sharded = world > 1 or args.sharded
-    if sharded:
-        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        os.environ.setdefault('MASTER_PORT', '29531')
-        os.environ.setdefault('RANK', str(rank))
-        os.environ.setdefault('WORLD_SIZE', str(world))
-        dist.init_process_group('nccl', device_id=dev)
+    if sharded and not dist.is_initialized():
+        _init_group(dev)
+    if SHARE_DEVICE and world > 1:
+        from stein_thinning import _native as nat
+        nat.lib().st_tune(5, 256 // world)   # the ranks' persistent grids must co-reside on one GPU
 
     cfg = CONFIGS[args.config]
     n, m = cfg['n'], cfg['m']
@@ -258,9 +290,7 @@ def main():
     launch_s = [e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]
     if sharded:
         dist.barrier()
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = _max_over_ranks([elapsed], dev)[0]
 
     if not sharded:
         result_idx = idx.cpu().numpy().view(np.uint32)
@@ -289,10 +319,7 @@ def main():
             avg = float(np.mean(launch_s))
             med = float(np.median(launch_s))
             if sharded:
-                import torch
-                tt = torch.tensor([avg, med], dtype=torch.float64, device=dev)
-                dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-                avg, med = (float(v) for v in tt.tolist())
+                avg, med = _max_over_ranks([avg, med], dev)
             pairs_launch = n * m / world          # per rank
             tflops = pairs_launch * flop_per_pair / avg / 1e12
             gins = pairs_launch * instr_per_pair / avg / 1e12
@@ -391,15 +418,9 @@ def main_ksd(args):
     import torch
     import torch.distributed as dist
     from stein_thinning import distributed as sd
-    rank = int(os.environ.get('RANK', 0))
-    world = int(os.environ.get('WORLD_SIZE', 1))
-    local = int(os.environ.get('LOCAL_RANK', 0))
-    torch.cuda.set_device(local)
-    dev = torch.device('cuda', local)
+    rank, world, dev = _setup_ranks()
     if world > 1:
-        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
-        os.environ.setdefault('MASTER_PORT', '29531')
-        dist.init_process_group('nccl', device_id=dev)
+        _init_group(dev)
     cfg = CONFIGS[args.config if args.config != 'c4' or args.ksd_full else 'c2']
     integrand, _, _ = make_integrand(cfg)
     n, d = cfg['n'], integrand.sample.shape[1]
@@ -414,7 +435,7 @@ def main_ksd(args):
     def run_once():
         c = be.colsum(a0, a1)
         if world > 1:
-            dist.all_reduce(c)
+            sd._all_reduce_sum(c)
         nat.check(L.st_ksd_finish(nat.ptr(p.x), nat.ptr(p.g), nat.ptr(p.w), n, p.ld, p.d, p.l, p.tr,
                                   nat.ptr(c), nat.ptr(ks), nat.stream_handle()), 'st_ksd_finish')
     for _ in range(args.warmup):
@@ -443,9 +464,7 @@ def main_ksd(args):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed, colsum_s], dtype=torch.float64, device=dev)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed, colsum_s = (float(v) for v in tt.tolist())
+        elapsed, colsum_s = _max_over_ranks([elapsed, colsum_s], dev)
     gf = integrand.weights is not None
     pairs = n * (n - 1) / 2
     rank_pairs = sum(n - 1 - a for a in range(a0, a1)) if n < 10 ** 4 else \
