@@ -53,6 +53,48 @@ def test_library_loads_and_types_without_gpu(libpath):
     assert lib.st_kernel_pairs(None, None, None, 8, 200, 1.0, 1.0, None, None, 1, None, None) == _native.ST_ERR_INVALID
 
 
+def test_host_side_validation_of_the_newer_entry_points(libpath):
+    """Argument checks that fail before any HIP call (no device needed): multi-GPU greedy, mailbox
+    sizing, KSD column sums, energy-distance column sums, host standardisation."""
+    import ctypes
+    from stein_thinning import _native
+    lib = _native.load_library(libpath)
+    inv = _native.ST_ERR_INVALID
+    assert lib.st_mailbox_bytes(1) > 0 and lib.st_mailbox_bytes(8) >= lib.st_mailbox_bytes(1)
+    assert lib.st_mailbox_bytes(0) == -1 and lib.st_mailbox_bytes(9) == -1
+    assert lib.st_ipc_handle_bytes() == 64
+    # st_greedy_sharded: NULL arrays, then nranks / rank / peer table / row range checks
+    args = [None, None, None, 10, 4, 16, 1.0, 4.0, 0, 10, 0, 2, None, 0, 5, None, None, None, 0, None]
+    assert lib.st_greedy_sharded(*args) == inv
+    buf = (ctypes.c_double * 64)()
+    p = ctypes.cast(buf, ctypes.c_void_p)
+    base = [p, p, None, 10, 4, 16, 1.0, 4.0, 0, 10, 0, 2, None, 0, 5, p, p, p, 1 << 20, None]
+    assert lib.st_greedy_sharded(*base) == inv                    # no peer table
+    assert b'peer' in lib.st_last_error()
+    table = (ctypes.c_void_p * 8)(p.value, p.value)
+    tp = ctypes.cast(table, ctypes.c_void_p)
+    for k, bad in [(11, 1), (11, 9), (10, 2), (8, 10), (9, 11)]:   # nranks 1 / 9, rank 2, row range
+        a = list(base)
+        a[12] = tp
+        a[k] = bad
+        assert lib.st_greedy_sharded(*a) == inv, (k, bad)
+    assert lib.st_mailbox_handshake(tp, 1, 0, 1, p, None) == inv
+    assert lib.st_mailbox_handshake(tp, 2, 0, 1 << 63, p, None) == inv
+    # KSD column sums / finish
+    assert lib.st_ksd_colsum(p, p, None, 10, 16, 4, 1.0, 4.0, 3, 2, p, None) == inv   # row_end < row_begin
+    assert lib.st_ksd_colsum(p, p, None, 10, 16, 4, 1.0, 4.0, 0, 11, p, None) == inv  # row_end > n
+    assert lib.st_ksd_finish(p, p, None, 10, 16, 4, 1.0, 4.0, None, p, None) == inv
+    # energy-distance column sums
+    assert lib.st_distance_colsum(p, 16, 10, p, 16, 10, 4, 0, 10, 0, None, None) == inv
+    assert lib.st_distance_colsum(p, 12, 10, p, 16, 10, 4, 0, 10, 0, p, None) == inv   # ld % 8
+    assert lib.st_distance_colsum(p, 16, 10, p, 16, 10, 4, 0, 11, 0, p, None) == inv   # range
+    assert lib.st_distance_colsum(p, 16, 10, None, 16, 10, 4, 0, 10, 1, p, None) == inv
+    assert lib.st_distance_colsum(p, 16, 10, p, 16, 10, 200, 0, 10, 0, p, None) == _native.ST_ERR_UNSUPPORTED
+    # host standardisation: bad arguments
+    status = ctypes.c_int32(0)
+    assert lib.st_standardize_host(None, None, 10, 4, 1, None, None, None, None, ctypes.byref(status)) == inv
+
+
 def test_library_is_gfx950_only(libpath):
     # the embedded code-object bundle names its target: amdgcn-amd-amdhsa--gfx950
     blob = open(libpath, 'rb').read()
