@@ -19,8 +19,8 @@ step() {  # step <name> <timeout_s> <cmd...>
 }
 MODE=${1:-all}
 if [[ $MODE == all || $MODE == test ]]; then
-  step smoke 600 python -c "import __graft_entry__ as g; g.smoke()"
-  step pytest_gpu 1200 python -m pytest tests -m gpu -x -q
+  step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
+  step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 fi
 if [[ $MODE == all || $MODE == bench ]]; then
   step bench 900 python bench.py --steps 3 --warmup 1
