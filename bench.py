@@ -251,22 +251,8 @@ def main():
             prob.greedy_launch(m, idx, a, ws)
     else:
         from stein_thinning import distributed as sd
-        runner = None
-        exchange_note = ''
-        if world > 1 and sd.device_exchange_eligible(d, world):
-            mb = sd.peer_mailboxes()
-            if mb.ok:
-                runner = sd.PersistentShardedGreedy(integrand, rank, world, m, mb)
-                probe_idx = runner.run()     # validates the device exchange end to end (untimed)
-                if not mb._agree(runner.completed(probe_idx)):
-                    runner, exchange_note = None, 'device exchange timed out; '
-            else:
-                exchange_note = f'device exchange unavailable ({mb.error}); '
-        if runner is None:
-            r0, r1 = sd.shard_bounds(n, rank, world)
-            backend = sd.HipShardBackend(integrand, r0, r1, world, m)
-            runner = sd.GraphedShardedGreedy(backend, m, use_graph=not args.no_graph)
-            runner.mode = exchange_note + 'rccl-' + runner.mode
+        # collective; completes one (untimed) validation run of the chosen exchange engine
+        runner = sd.sharded_runner(integrand, m, use_graph=not args.no_graph)
 
         def run_once():
             runner.launch()

@@ -287,6 +287,41 @@ int st_greedy_step(const double* x_soa, const double* g_soa, const double* weigh
                      "greedy publish launch");
 }
 
+int st_greedy_step_exchange(const double* x_soa, const double* g_soa, const double* weights,
+                            int64_t n, int32_t d, int64_t ld, double linv_scale, double linv_trace,
+                            int64_t row_offset, int64_t t, int32_t rank, int32_t nranks,
+                            void* const* peer_mailboxes, double* cands, uint32_t* idx_out,
+                            double* a_work, void* workspace, int64_t workspace_bytes,
+                            uint32_t* status_device, void* stream) {
+    int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
+    if (rc) return rc;
+    rc = check_peers(peer_mailboxes, nranks, rank);
+    if (rc) return rc;
+    if (t < 0) return fail(ST_ERR_INVALID, "t must be >= 0");
+    if (!cands || !a_work || !workspace || !status_device) return fail(ST_ERR_INVALID, "NULL output/workspace");
+    if (t > 0 && !idx_out) return fail(ST_ERR_INVALID, "idx_out is NULL");
+    if (row_offset < 0) return fail(ST_ERR_INVALID, "row_offset must be >= 0");
+    if (!aligned16(a_work) || !aligned16(workspace))
+        return fail(ST_ERR_INVALID, "a_work/workspace must be 16-byte aligned");
+    if (workspace_bytes < greedy_ws_bytes(d)) return fail(ST_ERR_INVALID, "workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    st::GreedyArgs a = make_args(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, a_work);
+    a.row_offset = row_offset;
+    a.t = t;
+    a.recs_in = cands;
+    a.nrecs_in = nranks;
+    a.recs_out = bank(workspace, d, 0);
+    a.idx_out = idx_out;
+    const int blocks = st::greedy_blocks(n, d);
+    rc = hip_check(st::launch_greedy_step(a, t == 0, blocks, s), "greedy step launch");
+    if (rc) return rc;
+    st::MailboxPeers peers{};
+    for (int r = 0; r < nranks; ++r) peers.p[r] = static_cast<uint64_t*>(peer_mailboxes[r]);
+    return hip_check(st::launch_greedy_rank_exchange(a.recs_out, blocks, a.rec_stride, d, peers, rank,
+                                                     nranks, t, cands, status_device, s),
+                     "rank exchange launch");
+}
+
 int st_greedy_finalize(const double* cands_in, int32_t nranks, int32_t d, uint32_t* idx_out,
                        int64_t t, void* stream) {
     if (!cands_in || !idx_out) return fail(ST_ERR_INVALID, "NULL pointer");

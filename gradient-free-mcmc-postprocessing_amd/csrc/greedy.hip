@@ -315,6 +315,88 @@ __global__ __launch_bounds__(kBlock) void greedy_publish(const double* __restric
     for (int k = threadIdx.x; k < 2 * d + 1 + kCandHeader; k += kBlock) out[k] = src[k];
 }
 
+// R > 1 ranks without RCCL: reduce this rank's K block records to the rank record (as
+// greedy_publish) and exchange the rank records through the peers' mailboxes (IPC-mapped uncached
+// device memory, system-scope stores over xGMI): every thread pushes words of the record into slot
+// `rank` of every peer, the block drains its stores, one flag word per peer follows; then lanes
+// r < nranks poll the flags of their own mailbox and the block copies the R records into recv
+// (rank order = np.argmin order of the concatenation, as the all-gather delivers).  Flags carry a
+// per-rank exchange counter kept in the own mailbox (the same on every rank: all ranks run the
+// same exchanges), so a graph replay never matches a stale flag; banks alternate with it, so a
+// slot is rewritten only after every rank has consumed it.  Bounded waits set status[0] = 1.
+__global__ __launch_bounds__(kBlock) void greedy_rank_exchange(const double* __restrict__ recs, int K,
+                                                              int64_t stride, int d,
+                                                              MailboxPeers peers, int rank,
+                                                              int nranks, int64_t t,
+                                                              double* __restrict__ recv,
+                                                              unsigned* status) {
+    __shared__ double s_v[kWaves];
+    __shared__ int64_t s_i[kWaves];
+    __shared__ int s_slot;
+    __shared__ int s_ok;
+    // an earlier exchange of this run timed out: finish the run without waiting again
+    if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != 0) return;
+    double v = INFINITY;
+    int64_t gi = INT64_MAX;
+    int slot = -1;
+    for (int r = threadIdx.x; r < K; r += kBlock) {
+        const double rv = recs[(int64_t)r * stride];
+        const int64_t ri = rec_gidx(recs + (int64_t)r * stride);
+        if (better(rv, ri, v, gi)) { v = rv; gi = ri; slot = r; }
+    }
+    double bv = v;
+    int64_t bi = gi;
+    block_minloc(bv, bi, s_v, s_i);
+    if (slot >= 0 && gi == bi) s_slot = slot;
+    __syncthreads();
+    const double* src = recs + (int64_t)s_slot * stride;
+    uint64_t* inbox = peers.p[rank];
+    const uint64_t count = __hip_atomic_load(inbox + kMailboxXchgCount, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_SYSTEM);
+    const uint64_t flag = count + 1;   // never 0 (the zeroed mailbox) and never reused
+    const int64_t bank = (int64_t)(count & 1) * kMailboxRanks;
+    auto slot_of = [&](uint64_t* mb, int r) { return mb + kMailboxRecBase + (bank + r) * kMailboxRecSlotWords; };
+    for (int64_t k = threadIdx.x; k < stride; k += kBlock) {
+        const uint64_t w = (uint64_t)__double_as_longlong(src[k]);
+        for (int p = 0; p < nranks; ++p)
+            __hip_atomic_store(slot_of(peers.p[p], rank) + 8 + k, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // every word of the record has landed
+    __syncthreads();
+    if (threadIdx.x == 0)
+        for (int p = 0; p < nranks; ++p)
+            __hip_atomic_store(slot_of(peers.p[p], rank), flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (threadIdx.x < 64) {
+        const int lane = threadIdx.x;
+        bool got = lane >= nranks;
+        const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t limit = t == 0 ? 1000000000ull : 200000000ull;   // 10 s at a run's start, else 2 s
+        int ok = 1;
+        for (unsigned it = 0;; ++it) {
+            if (!got)
+                got = __hip_atomic_load(slot_of(inbox, lane), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == flag;
+            if (__all(got)) break;
+            __builtin_amdgcn_s_sleep(1);
+            if ((it & 15) == 15 && __any(__builtin_amdgcn_s_memrealtime() - t0 > limit)) { ok = 0; break; }
+        }
+        if (lane == 0) s_ok = ok;
+    }
+    __syncthreads();
+    if (!s_ok) {
+        if (threadIdx.x == 0) __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return;
+    }
+    for (int64_t e = threadIdx.x; e < (int64_t)nranks * stride; e += kBlock) {
+        const int r = (int)(e / stride);
+        const int64_t k = e - (int64_t)r * stride;
+        recv[e] = __longlong_as_double((long long)__hip_atomic_load(slot_of(inbox, r) + 8 + k, __ATOMIC_RELAXED,
+                                                                    __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+    // every flag of this exchange has been seen: advance the counter (own mailbox, this rank only)
+    if (threadIdx.x == 0)
+        __hip_atomic_store(inbox + kMailboxXchgCount, count + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // K3: idx[t] from the K records of the last launch (or the last all-gather).
 __global__ __launch_bounds__(kBlock) void greedy_finalize(const double* __restrict__ recs, int K,
                                                          int64_t stride, uint32_t* idx_out,
@@ -436,6 +518,13 @@ hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStr
 hipError_t launch_greedy_publish(const double* recs, int K, int64_t stride, int d, double* out,
                                  hipStream_t s) {
     greedy_publish<<<1, kBlock, 0, s>>>(recs, K, stride, d, out);
+    return hipGetLastError();
+}
+
+hipError_t launch_greedy_rank_exchange(const double* recs, int K, int64_t stride, int d,
+                                       const MailboxPeers& peers, int rank, int nranks, int64_t t,
+                                       double* recv, unsigned* status, hipStream_t s) {
+    greedy_rank_exchange<<<1, kBlock, 0, s>>>(recs, K, stride, d, peers, rank, nranks, t, recv, status);
     return hipGetLastError();
 }
 

@@ -86,8 +86,8 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
         bool nan = false, inf = false;
         for (int64_t e = total * t / T; e < total * (t + 1) / T; ++e) {
             const double xv = sample[e], gv = gradient[e];
-            nan |= (xv != xv) | (gv != gv);
-            inf |= (fabs(xv) == INFINITY) | (fabs(gv) == INFINITY);
+            nan |= (int)(xv != xv) | (int)(gv != gv);
+            inf |= (int)(fabs(xv) == INFINITY) | (int)(fabs(gv) == INFINITY);
         }
         nanf[t] = nan;
         inff[t] = inf;

@@ -10,12 +10,19 @@ constexpr int kMaxCtDim = 8;     // compile-time-d kernels for d <= 8
 constexpr int kMaxBlocks = 1024; // greedy step grid cap (4 x 256-thread blocks per CU)
 constexpr int kCandHeader = 2;   // candidate record: {val, gidx(bits)} then x[d], g[d], w
 constexpr int64_t kWsControlBytes = 8 * 128 + 128;   // persistent kernel: arrival counters + status
-// peer mailbox of the multi-rank persistent kernel (u64 words): 2 banks x kMailboxRanks slots x
-// 2 granules, then kMailboxRanks handshake words
+// peer mailbox (u64 words), one per rank, uncached device memory:
+//   [0, 32)        persistent kernel: 2 banks x kMailboxRanks slots x 2 tagged granules
+//   [32, 40)       handshake words (one per rank)
+//   [40]           exchange counter of the step-kernel path (written by this rank only)
+//   [64, ...)      step-kernel path: 2 banks x kMailboxRanks record slots, each a flag word then
+//                  the candidate record (cand_stride(d) doubles) at word 8
 constexpr int kMailboxRanks = 8;
 constexpr int kMailboxHandshake = 2 * kMailboxRanks * 2;
-constexpr int64_t kMailboxBytes = 512;
-static_assert((kMailboxHandshake + kMailboxRanks) * 8 <= kMailboxBytes, "mailbox layout");
+constexpr int kMailboxXchgCount = kMailboxHandshake + kMailboxRanks;
+constexpr int kMailboxRecBase = 64;
+constexpr int kMailboxRecSlotWords = 272;   // 8 header words + cand_stride(kMaxDim) = 260, 64-B multiple
+constexpr int64_t kMailboxBytes = (int64_t)(kMailboxRecBase + 2 * kMailboxRanks * kMailboxRecSlotWords) * 8;
+static_assert(kMailboxXchgCount < kMailboxRecBase, "mailbox layout");
 
 struct MailboxPeers {
     uint64_t* p[kMailboxRanks];
@@ -31,6 +38,7 @@ struct RankSpec {
 };
 
 inline int64_t cand_stride(int d) { return ((kCandHeader + 2 * d + 1) + 1) & ~int64_t(1); }
+static_assert(8 + ((kCandHeader + 2 * kMaxDim + 1) + 1) / 2 * 2 <= kMailboxRecSlotWords, "record slot");
 
 struct GreedyArgs {
     const double* x;      // SoA (d, ld) standardised sample shard
@@ -66,6 +74,9 @@ hipError_t launch_greedy_publish(const double* recs, int K, int64_t stride, int 
                                  hipStream_t s);
 hipError_t launch_greedy_finalize(const double* recs, int K, int64_t stride, uint32_t* idx_out,
                                   int64_t t, hipStream_t s);
+hipError_t launch_greedy_rank_exchange(const double* recs, int K, int64_t stride, int d,
+                                       const MailboxPeers& peers, int rank, int nranks, int64_t t,
+                                       double* recv, unsigned* status, hipStream_t s);
 
 struct PairArgs {
     const double* x;

@@ -3,16 +3,19 @@
 The reference has no multi-device path (its only parallelism is joblib / Dask fan-out over chains,
 ``code/src/utils/parallel.py:18-52``).  Here the candidate axis n of one greedy run is split into
 contiguous row blocks, one per rank; every rank picks the same winner per step (lowest value, then
-lowest global index, NaN first: np.argmin over the concatenated array).  Two exchange engines:
+lowest global index, NaN first: np.argmin over the concatenated array).  Three exchange engines
+(``exchange_engine``; ``sharded_runner`` picks, validates and falls back):
 
-* ``PersistentShardedGreedy`` (d = 2, 4; default): every rank holds the full standardised arrays
+* ``PersistentShardedGreedy`` (d = 2, 4): every rank holds the full standardised arrays
   (replicated, read-only) and runs ONE persistent launch over its row block; per step the ranks
   exchange their local winners {A_min, global index} through IPC-mapped device mailboxes (xGMI
   stores, no host round trip, no collective launch).  Handles are exchanged once with
   ``torch.distributed`` and the round trip is verified by a handshake before first use.
-* ``GraphedShardedGreedy`` (any d; fallback): per step a fused kernel over the shard, ONE candidate
-  record {value, global index, x row, g row, w} per rank, RCCL ``all_gather_into_tensor`` of the
-  records, the m-step loop captured once into a HIP graph.
+* device-exchange steps (other d): per step a fused kernel over the shard, ONE candidate record
+  {value, global index, x row, g row, w} per rank, exchanged by a one-block mailbox kernel
+  (st_greedy_step_exchange); the m-step loop is captured once into a HIP graph.
+* ``GraphedShardedGreedy`` with RCCL (any d; fallback, or ST_SHARDED_EXCHANGE=rccl): the same
+  records, RCCL ``all_gather_into_tensor`` per step, also graph-captured.
 
 No n-length vector crosses xGMI in either; the design choice vs. an all-reduce of the n-length
 column-sum vector is recorded in DESIGN.md (that all-reduce is used by the full-sample KSD).
@@ -40,9 +43,12 @@ def shard_bounds(n: int, rank: int, world: int):
 
 
 class HipShardBackend:
-    """Device state of one rank's shard + the C-ABI step/finalize launches."""
+    """Device state of one rank's shard + the C-ABI step/finalize launches.  With ``mailboxes``
+    (a verified PeerMailboxes set) each step also exchanges the rank records device-side
+    (st_greedy_step_exchange) and no collective is issued."""
 
-    def __init__(self, integrand: SteinIntegrand, r0: int, r1: int, nranks: int, n_points: int):
+    def __init__(self, integrand: SteinIntegrand, r0: int, r1: int, nranks: int, n_points: int,
+                 mailboxes: Optional['PeerMailboxes'] = None, rank: int = 0):
         import torch
         from .device import DeviceProblem
         self.device = nat.require_device()
@@ -57,9 +63,19 @@ class HipShardBackend:
         self.idx = torch.zeros(n_points, dtype=torch.int32, device=self.device)
         self.send = torch.zeros(self.stride, dtype=torch.float64, device=self.device)
         self.recv = torch.zeros(self.stride * nranks, dtype=torch.float64, device=self.device)
+        self.mb, self.rank = mailboxes, int(rank)
+        self.device_exchange = mailboxes is not None
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
 
     def step(self, t: int) -> None:
         p = self.prob
+        if self.device_exchange:
+            nat.check(nat.lib().st_greedy_step_exchange(
+                nat.ptr(p.x), nat.ptr(p.g), nat.ptr(p.w), p.n, p.d, p.ld, p.l, p.tr, self.r0, t,
+                self.rank, self.nranks, self.mb.table_ptr(), nat.ptr(self.recv), nat.ptr(self.idx),
+                nat.ptr(self.a), nat.ptr(self.ws), self.ws.numel() * 8, nat.ptr(self.status),
+                nat.stream_handle()), 'st_greedy_step_exchange')
+            return
         nat.check(nat.lib().st_greedy_step(
             nat.ptr(p.x), nat.ptr(p.g), nat.ptr(p.w), p.n, p.d, p.ld, p.l, p.tr, self.r0, t,
             self.nranks, nat.ptr(self.recv), nat.ptr(self.send), nat.ptr(self.idx),
@@ -73,6 +89,10 @@ class HipShardBackend:
 
     def indices(self) -> np.ndarray:
         return self.idx.cpu().numpy().view(np.uint32).copy()
+
+    def exchange_ok(self) -> bool:
+        """No bounded wait of the device exchange expired (always True on the RCCL path)."""
+        return int(self.status.item()) == 0
 
 
 def _all_gather(recv, send, group=None) -> None:
@@ -90,9 +110,12 @@ def _all_gather(recv, send, group=None) -> None:
 
 def _sharded_loop(backend, n_points: int, group=None) -> None:
     import torch.distributed as dist
+    exchanged = getattr(backend, 'device_exchange', False)   # the step call exchanged already
     collective = dist.is_available() and dist.is_initialized()
     for t in range(n_points):
         backend.step(t)
+        if exchanged:
+            continue
         if collective:
             _all_gather(backend.recv, backend.send, group)
         else:
@@ -153,6 +176,9 @@ class GraphedShardedGreedy:
             self.graph.replay()
         else:
             _sharded_loop(self.backend, self.n_points, self.group)
+
+    def indices(self) -> np.ndarray:
+        return self.backend.indices()
 
     def run(self) -> np.ndarray:
         self.launch()
@@ -270,11 +296,19 @@ def peer_mailboxes(group=None) -> PeerMailboxes:
     return mb
 
 
+def exchange_engine(d: int, world: int) -> str:
+    """Engine of a ``world``-rank run at dimension d: 'persistent' (d = 2, 4: one persistent launch
+    per rank, winners exchanged in-kernel), 'steps' (other d: launch-per-step kernels in a HIP graph,
+    records exchanged by a mailbox kernel), or 'rccl' (RCCL all-gather per step; forced by
+    ST_SHARDED_EXCHANGE=rccl, and the fallback when the mailboxes cannot be set up)."""
+    if not 2 <= world <= MAX_PEER_RANKS or os.environ.get('ST_SHARDED_EXCHANGE', 'device') == 'rccl':
+        return 'rccl'
+    return 'persistent' if d in (2, 4) else 'steps'
+
+
 def device_exchange_eligible(d: int, world: int) -> bool:
-    """Whether the persistent multi-rank kernel serves this run (ST_SHARDED_EXCHANGE=rccl forces
-    the RCCL path)."""
-    return (d in (2, 4) and 2 <= world <= MAX_PEER_RANKS
-            and os.environ.get('ST_SHARDED_EXCHANGE', 'device') != 'rccl')
+    """Whether a mailbox (device-side) exchange engine serves this run."""
+    return exchange_engine(d, world) != 'rccl'
 
 
 class PersistentShardedGreedy:
@@ -425,6 +459,67 @@ def thin_gf_sharded(sample, log_p, log_q, gradient_q, n_points: int, standardize
     return _thin_sharded_integrand(integrand, n_points, group)
 
 
+class _EagerRecords:
+    """Records all-gathered per step from Python (gloo process group with device buffers: tests)."""
+
+    mode = 'records-all-gather'
+
+    def __init__(self, backend: HipShardBackend, n_points: int, group=None):
+        self.backend, self.n_points, self.group = backend, n_points, group
+        self.launch()
+
+    def launch(self) -> None:
+        _sharded_loop(self.backend, self.n_points, self.group)
+
+    def indices(self) -> np.ndarray:
+        return self.backend.indices()
+
+    def run(self) -> np.ndarray:
+        self.launch()
+        return self.indices()
+
+
+def sharded_runner(integrand: SteinIntegrand, n_points: int, group=None, use_graph: bool = True):
+    """Collective: build this rank's runner for a row-sharded greedy run and complete one run with
+    it (the validation run; its result is ``runner.indices()``).  Tries the device-exchange engine
+    (exchange_engine) first; if any rank's bounded wait expired, every rank falls back to RCCL.
+    ``runner.mode`` names the engine; ``runner.launch()`` enqueues a further run."""
+    import torch.distributed as dist
+    rank, world = _world(group)
+    d = integrand.sample.shape[1]
+    engine = exchange_engine(d, world)
+    note = ''
+    if engine != 'rccl':
+        mb = peer_mailboxes(group)
+        if mb.ok:
+            if engine == 'persistent':
+                runner = PersistentShardedGreedy(integrand, rank, world, n_points, mb)
+                runner.launch()
+                ok = runner.completed()
+            else:
+                r0, r1 = shard_bounds(integrand.n, rank, world)
+                backend = HipShardBackend(integrand, r0, r1, world, n_points, mailboxes=mb, rank=rank)
+                runner = GraphedShardedGreedy(backend, n_points, group, use_graph)
+                runner.mode = 'device-exchange-steps-' + runner.mode
+                ok = backend.exchange_ok()
+            if mb._agree(ok):
+                return runner
+            mb.ok = False   # a bounded wait expired somewhere: RCCL path from now on
+            mb.error = f'{engine} device exchange timed out'
+            note = 'device exchange timed out; '
+        else:
+            note = f'device exchange unavailable ({mb.error}); '
+    r0, r1 = shard_bounds(integrand.n, rank, world)
+    backend = HipShardBackend(integrand, r0, r1, world, n_points)
+    if dist.is_initialized() and dist.get_backend(group) == 'nccl':
+        runner = GraphedShardedGreedy(backend, n_points, group, use_graph)
+        runner.mode = note + 'rccl-' + runner.mode
+        return runner
+    runner = _EagerRecords(backend, n_points, group)
+    runner.mode = note + runner.mode
+    return runner
+
+
 def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None,
                             use_graph: bool = True) -> np.ndarray:
     n_points = int(n_points)
@@ -434,25 +529,9 @@ def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None
     if world > integrand.n:
         raise ValueError(f'{world} ranks for {integrand.n} rows: every rank needs at least one row')
     global last_mode
-    import torch.distributed as dist
-    if world > 1 and device_exchange_eligible(integrand.sample.shape[1], world):
-        mb = peer_mailboxes(group)
-        if mb.ok:
-            runner = PersistentShardedGreedy(integrand, rank, world, n_points, mb)
-            idx = runner.run()
-            if mb._agree(runner.completed(idx)):
-                last_mode = runner.mode
-                return idx
-            mb.ok = False   # a bounded wait expired somewhere: RCCL path from now on
-            mb.error = 'persistent run timed out'
-    r0, r1 = shard_bounds(integrand.n, rank, world)
-    backend = HipShardBackend(integrand, r0, r1, world, n_points)
-    if dist.is_initialized() and dist.get_backend(group) == 'nccl':
-        runner = GraphedShardedGreedy(backend, n_points, group, use_graph)
-        last_mode = f'rccl-{runner.mode}'
-        return runner.run()
-    last_mode = 'records-all-gather'
-    return run_sharded(backend, n_points, group)
+    runner = sharded_runner(integrand, n_points, group, use_graph)
+    last_mode = runner.mode
+    return runner.indices()
 
 
 last_mode = None   # exchange engine of the last sharded thin in this process (tests / bench)

@@ -140,6 +140,25 @@ int st_greedy_sharded(const double *x_soa, const double *g_soa, const double *we
                       void *const *peer_mailboxes, uint64_t seq_base, int64_t n_points,
                       uint32_t *idx_out, double *a_work, void *workspace,
                       int64_t workspace_bytes, void *stream);
+/*
+ * Any d (the launch-per-step path of st_greedy_step) with the per-step rank exchange through the
+ * same mailboxes instead of an RCCL all-gather: one call = the step kernel over this rank's shard
+ * + a one-block exchange kernel that pushes this rank's candidate record into slot `rank` of every
+ * peer's mailbox and collects the nranks records of this step into cands (nranks * stride
+ * doubles; the next call's input, as st_greedy_step's cands_in).  No host synchronisation or
+ * collective inside, so the m-step loop can be captured into one HIP graph and replayed; flags
+ * carry a device-side exchange counter, so replays never see stale records.  All ranks must make
+ * the same sequence of calls.  A peer that does not answer within the bounded wait (10 s at t = 0,
+ * 2 s otherwise) sets status_device[0] = 1; later exchanges then return at once (the indices of
+ * that run are garbage and the mailbox set must not be reused).  Finish with st_greedy_finalize
+ * (cands, nranks).
+ */
+int st_greedy_step_exchange(const double *x_soa, const double *g_soa, const double *weights,
+                            int64_t n, int32_t d, int64_t ld, double linv_scale, double linv_trace,
+                            int64_t row_offset, int64_t t, int32_t rank, int32_t nranks,
+                            void *const *peer_mailboxes, double *cands, uint32_t *idx_out,
+                            double *a_work, void *workspace, int64_t workspace_bytes,
+                            uint32_t *status_device, void *stream);
 
 /* ------------------------------------------------------------------------------------------
  * Integrand protocol -- replaces integrand(ind1, ind2) of the closures returned by

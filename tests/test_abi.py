@@ -78,6 +78,15 @@ def test_host_side_validation_of_the_newer_entry_points(libpath):
         a[12] = tp
         a[k] = bad
         assert lib.st_greedy_sharded(*a) == inv, (k, bad)
+    # st_greedy_step_exchange: peer table / status checks
+    step = [p, p, None, 10, 9, 16, 1.0, 4.0, 0, 0, 0, 2, None, p, p, p, p, 1 << 20, p, None]
+    assert lib.st_greedy_step_exchange(*step) == inv               # no peer table
+    step[12] = tp
+    step[18] = None
+    assert lib.st_greedy_step_exchange(*step) == inv               # no status word
+    step[18] = p
+    step[16] = None
+    assert lib.st_greedy_step_exchange(*step) == inv               # no workspace
     assert lib.st_mailbox_handshake(tp, 1, 0, 1, p, None) == inv
     assert lib.st_mailbox_handshake(tp, 2, 0, 1 << 63, p, None) == inv
     # KSD column sums / finish

@@ -1,6 +1,7 @@
-"""Multi-process sharded thinning on the GPU box: 2 ranks (processes) on the one visible GPU,
-exchanging candidate records through gloo (RCCL cannot place two ranks on one device), and a
-1-rank RCCL run of the HIP-graph-captured loop (step + publish + all-gather per step)."""
+"""Multi-process sharded thinning on the GPU box: 2-3 ranks (processes) on the one visible GPU
+(RCCL cannot place two ranks on one device, so the group is gloo): the record all-gather path, the
+persistent device-exchange engine (d = 2, 4) and the launch-per-step device-exchange engine (other
+d) through IPC-mapped mailboxes, and a 1-rank RCCL run of the HIP-graph-captured loop."""
 import os
 import socket
 
@@ -25,9 +26,9 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _data():
+def _data(d=4):
     rng = np.random.default_rng(5)
-    n, d = 40_003, 4
+    n = 40_003
     x = rng.normal(size=(n, d))
     x[30_000:30_400] = x[2_000:2_400]      # exact ties across the shard boundary
     g = -x + 0.1 * rng.normal(size=(n, d))
@@ -37,14 +38,14 @@ def _data():
     return x, g, log_p, log_q
 
 
-def _worker(rank, world, port, backend, gf, out_dir, exchange='device', runs=1):
+def _worker(rank, world, port, backend, gf, out_dir, exchange='device', runs=1, d=4):
     os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE=exchange)
     torch.cuda.set_device(0)
     kw = dict(device_id=torch.device('cuda', 0)) if backend == 'nccl' else {}
     dist.init_process_group(backend, rank=rank, world_size=world, **kw)
     try:
         from stein_thinning import distributed as sd
-        x, g, log_p, log_q = _data()
+        x, g, log_p, log_q = _data(d)
         for run in range(runs):
             gf_run = gf if run % 2 == 0 else not gf   # alternate kernels on the same mailboxes
             if gf_run:
@@ -58,8 +59,8 @@ def _worker(rank, world, port, backend, gf, out_dir, exchange='device', runs=1):
         dist.destroy_process_group()
 
 
-def _want(gf):
-    x, g, log_p, log_q = _data()
+def _want(gf, d=4):
+    x, g, log_p, log_q = _data(d)
     return o.thin_gf(x, log_p, log_q, g, 80, preconditioner='med') if gf else o.thin(x, g, 80, preconditioner='med')
 
 
@@ -87,7 +88,53 @@ def test_device_exchange_processes_share_one_gpu(tmp_path, world, gf):
             np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
 
 
+@pytest.mark.parametrize('world,gf,d', [(2, False, 3), (3, True, 10)])
+def test_step_device_exchange_processes_share_one_gpu(tmp_path, world, gf, d):
+    """Launch-per-step engine with the mailbox exchange kernel (d outside the persistent kernel's
+    set; compile-time-d and runtime-d step kernels): graph-captured loop, three consecutive runs on
+    the same mailboxes (the device-side exchange counter carries over replays), both kernels."""
+    mp.spawn(_worker, args=(world, _free_port(), 'gloo', gf, str(tmp_path), 'device', 3, d), nprocs=world,
+             join=True)
+    for run in range(3):
+        want = _want(gf if run % 2 == 0 else not gf, d)
+        for r in range(world):
+            assert (tmp_path / f'mode{r}_{run}.txt').read_text() == 'device-exchange-steps-graph'
+            np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
+
+
 def test_single_rank_rccl_graph_capture(tmp_path):
     mp.spawn(_worker, args=(1, _free_port(), 'nccl', False, str(tmp_path)), nprocs=1, join=True)
     x, g, _, _ = _data()
     np.testing.assert_array_equal(np.load(tmp_path / 'idx0_0.npy'), o.thin(x, g, 80, preconditioner='med'))
+
+
+def _small_worker(rank, world, port, out_dir, exchange, d):
+    """Tiny shards (n = 901 over `world` ranks: one block per rank) and m > n (2 000 points, the
+    Gaussian_mixture.ipynb m = 10 000 > n = 1 000 regime): repeated selections, both kernels."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE=exchange)
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from stein_thinning import distributed as sd
+        rng = np.random.default_rng(3)
+        x = rng.normal(size=(901, d))
+        g = -x
+        idx = sd.thin_sharded(x, g, 2000, preconditioner='med')
+        np.save(os.path.join(out_dir, f'small{rank}.npy'), idx)
+        with open(os.path.join(out_dir, f'smallmode{rank}.txt'), 'w') as f:
+            f.write(str(sd.last_mode))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,exchange,d', [(3, 'device', 2), (3, 'device', 5), (2, 'rccl', 2)])
+def test_tiny_shards_and_more_points_than_rows(tmp_path, world, exchange, d):
+    mp.spawn(_small_worker, args=(world, _free_port(), str(tmp_path), exchange, d), nprocs=world, join=True)
+    rng = np.random.default_rng(3)
+    x = rng.normal(size=(901, d))
+    want = o.thin(x, -x, 2000, preconditioner='med')
+    expect = {'rccl': 'records-all-gather', 'device': 'device-exchange' if d in (2, 4) else
+              'device-exchange-steps-graph'}[exchange]
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f'small{r}.npy'), want)
+        assert (tmp_path / f'smallmode{r}.txt').read_text() == expect
