@@ -1,5 +1,6 @@
 // C ABI (include/stein_thinning_hip.h): argument validation, workspace carving, launch sequencing.
 // No allocation, no synchronisation: every entry point only enqueues work on the caller's stream.
+#include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -320,6 +321,20 @@ int st_greedy_step_exchange(const double* x_soa, const double* g_soa, const doub
     return hip_check(st::launch_greedy_rank_exchange(a.recs_out, blocks, a.rec_stride, d, peers, rank,
                                                      nranks, t, cands, status_device, s),
                      "rank exchange launch");
+}
+
+int st_proxy_logpdf_grad(const double* x, int64_t n, int32_t d, const double* loc,
+                         const double* whiten, const double* precision, double df, double c_log,
+                         double* log_q_out, double* grad_out, void* stream) {
+    if (n < 0) return fail(ST_ERR_INVALID, "n must be >= 0");
+    if (d < 1) return fail(ST_ERR_INVALID, "d must be >= 1");
+    if (d > st::kMaxDim) return fail(ST_ERR_UNSUPPORTED, "d = %d exceeds %d", d, st::kMaxDim);
+    if (!(df >= 0.0) || df == INFINITY) return fail(ST_ERR_INVALID, "df must be 0 (Gaussian) or finite > 0");
+    if (n == 0) return ST_OK;
+    if (!x || !loc || !whiten || !precision || !log_q_out || !grad_out)
+        return fail(ST_ERR_INVALID, "NULL pointer");
+    st::ProxyArgs a{x, loc, whiten, precision, n, d, df, c_log, log_q_out, grad_out};
+    return hip_check(st::launch_proxy(a, static_cast<hipStream_t>(stream)), "proxy launch");
 }
 
 int st_greedy_finalize(const double* cands_in, int32_t nranks, int32_t d, uint32_t* idx_out,

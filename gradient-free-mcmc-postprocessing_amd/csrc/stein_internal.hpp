@@ -74,6 +74,21 @@ hipError_t launch_greedy_publish(const double* recs, int K, int64_t stride, int 
                                  hipStream_t s);
 hipError_t launch_greedy_finalize(const double* recs, int K, int64_t stride, uint32_t* idx_out,
                                   int64_t t, hipStream_t s);
+struct ProxyArgs {
+    const double* x;     // row-major (n, d) raw sample
+    const double* loc;   // (d)
+    const double* U;     // (d, d) row-major, scipy _PSD factor: maha = |(x - loc) @ U|^2
+    const double* P;     // (d, d) row-major, np.linalg.inv(cov / shape)
+    int64_t n;
+    int d;
+    double df;           // 0: Gaussian; > 0: Student-t degrees of freedom
+    double c_log;        // Gaussian: rank*log(2 pi) + log_pdet; t: A - B - C - D
+    double* log_q;       // (n)
+    double* grad;        // row-major (n, d)
+};
+int64_t proxy_lds_bytes(int d);
+hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s);
+
 hipError_t launch_greedy_rank_exchange(const double* recs, int K, int64_t stride, int d,
                                        const MailboxPeers& peers, int rank, int nranks, int64_t t,
                                        double* recv, unsigned* status, hipStream_t s);

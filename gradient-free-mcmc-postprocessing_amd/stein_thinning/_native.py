@@ -73,6 +73,8 @@ SIGNATURES = {
     'st_greedy_step_exchange': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
                                                _i64, _i64, _i32, _i32, _c_dp, _c_dp, _c_dp, _c_dp,
                                                _c_dp, _i64, _c_dp, _c_dp]),
+    'st_proxy_logpdf_grad': (ctypes.c_int, [_c_dp, _i64, _i32, _c_dp, _c_dp, _c_dp, _f64, _f64, _c_dp,
+                                            _c_dp, _c_dp]),
 }
 ABI_VERSION = 1
 

@@ -161,6 +161,22 @@ int st_greedy_step_exchange(const double *x_soa, const double *g_soa, const doub
                             uint32_t *status_device, void *stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Proxy producers for thin_gf -- replaces the O(n d^2) host prep of
+ *   gaussian_thin (code/src/thinning.py:15-16): scipy.stats.multivariate_normal.logpdf(x, mean,
+ *     cov) and -np.einsum('ij,kj->ki', np.linalg.inv(cov), x - mean)           (df = 0)
+ *   thin_gf_t (Gradient_free_Student_t.ipynb cells 29, 31, 40): scipy.stats.multivariate_t.logpdf
+ *     (x, loc, shape, df) and t_grad_log_pdf(x, loc, shape, df)                (df > 0)
+ * x: row-major (n, d) device array (the caller's NumPy layout); loc (d); whiten (d, d) row-major =
+ * scipy's _PSD(cov).U; precision (d, d) row-major = np.linalg.inv(cov); c_log = rank * log(2 pi) +
+ * log_pdet (Gaussian) or A - B - C - D of scipy's multivariate_t._logpdf (t).  Writes log_q_out (n)
+ * and grad_out (row-major (n, d)).  Per-row dot products are summed in a different order than
+ * NumPy/BLAS (fp64 tolerance, not bit-identical).
+ * ---------------------------------------------------------------------------------------- */
+int st_proxy_logpdf_grad(const double *x, int64_t n, int32_t d, const double *loc,
+                         const double *whiten, const double *precision, double df, double c_log,
+                         double *log_q_out, double *grad_out, void *stream);
+
+/* ------------------------------------------------------------------------------------------
  * Integrand protocol -- replaces integrand(ind1, ind2) of the closures returned by
  * stein_thinning.thinning._make_stein_integrand / _make_stein_gf_integrand and
  * stein_thinning.kernel.vfk0_imq (restated at JAX_Stein_Thinning.ipynb cell 27, json ~354-361;

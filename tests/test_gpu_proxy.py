@@ -1,0 +1,92 @@
+"""Proxy producers on the GPU (csrc/proxy.hip via st_proxy_logpdf_grad) against the reference's
+scipy computations (oracle/proxy_numpy.py): log q and grad log q to fp64 rounding (relative 1e-12;
+the per-row dot products are summed in a different order than BLAS), and the downstream selections
+of gaussian_thin / thin_gf_t identical to the reference's."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+if not torch.cuda.is_available():
+    pytest.skip('no HIP device', allow_module_level=True)
+
+from oracle import proxy_numpy as op  # noqa: E402
+from oracle.models import gm_reference_sample  # noqa: E402
+from stein_thinning import proxy  # noqa: E402
+
+RTOL = 1e-12
+
+
+def _close(got, want):
+    scale = max(float(np.abs(want).max()), 1.0) if want.size else 1.0
+    np.testing.assert_allclose(got, want, rtol=RTOL, atol=RTOL * scale)
+
+
+def _case(n, d, seed):
+    rng = np.random.default_rng(seed)
+    a = rng.normal(size=(d, d))
+    cov = a @ a.T / d + 0.3 * np.eye(d)
+    mean = rng.normal(size=d)
+    x = mean + rng.normal(size=(n, d)) @ np.linalg.cholesky(cov).T * 1.5
+    return x, mean, cov
+
+
+@pytest.mark.parametrize('d', [1, 2, 3, 4, 7, 8, 16, 50, 65, 128])
+@pytest.mark.parametrize('n', [1, 63, 64, 65, 5000])
+def test_gaussian_proxy_matches_scipy(n, d):
+    x, mean, cov = _case(n, d, 10 * d + n)
+    lq, gq = proxy.gaussian_proxy(x, mean, cov)
+    wl, wg = op.gaussian_proxy(x, mean, cov)
+    assert lq.shape == (n,) and gq.shape == (n, d)
+    _close(lq, np.atleast_1d(wl))
+    _close(gq, wg)
+
+
+@pytest.mark.parametrize('d', [1, 2, 4, 9, 50, 128])
+@pytest.mark.parametrize('df', [1.0, 3.0, 4.0, 30.5])
+def test_student_t_proxy_matches_scipy_and_notebook_gradient(d, df):
+    x, loc, shape = _case(777, d, d + int(df * 10))
+    lq, gq = proxy.student_t_proxy(x, loc, shape * 3, df)
+    wl, wg = op.student_t_proxy(x, loc, shape * 3, df)
+    _close(lq, wl)
+    _close(gq, wg)
+
+
+def test_empty_sample():
+    lq, gq = proxy.gaussian_proxy(np.zeros((0, 3)), np.zeros(3), np.eye(3))
+    assert lq.shape == (0,) and gq.shape == (0, 3)
+
+
+def test_gaussian_thin_selects_the_reference_points_gm():
+    sample, _, logpdf, _ = gm_reference_sample()
+    log_p = logpdf(sample)
+    mean = np.mean(sample, axis=0)
+    cov = np.cov(sample, rowvar=False, ddof=2)
+    got = proxy.gaussian_thin(sample, log_p, mean, cov, 40)
+    want = op.gaussian_thin(sample, log_p, mean, cov, 40)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_thin_gf_t_selects_the_reference_points_gm():
+    sample, _, logpdf, _ = gm_reference_sample()
+    log_p = logpdf(sample)
+    cov = np.cov(sample, rowvar=False, ddof=2)
+    mode = sample[np.argmax(log_p)]
+    got = proxy.thin_gf_t(sample, log_p, mode, cov * 3, 4, 100)
+    want = op.thin_gf_t(sample, log_p, mode, cov * 3, 4, 100)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_gaussian_thin_selects_the_reference_points_d50():
+    rng = np.random.default_rng(12349)
+    d, n = 50, 4000
+    idx = np.arange(d)
+    cov = 0.5 ** np.abs(idx[:, None] - idx[None, :])
+    x = rng.normal(size=(n, d)) @ np.linalg.cholesky(cov).T
+    log_p = -0.5 * np.einsum('ij,jk,ik->i', x, np.linalg.inv(cov), x)
+    mean = x.mean(axis=0)
+    qcov = 1.2 * np.cov(x, rowvar=False)
+    got = proxy.gaussian_thin(x, log_p, mean, qcov, 60)
+    want = op.gaussian_thin(x, log_p, mean, qcov, 60)
+    np.testing.assert_array_equal(got, want)
