@@ -221,12 +221,15 @@ def main():
     ap.add_argument('--no-graph', action='store_true', help='N > 1: eager per-step launches instead of a HIP graph')
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
-    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd'],
+    ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
+    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
                          '(row-sharded, RCCL all-reduce of the n-length column-sum vector)')
     args = ap.parse_args()
     if args.workload == 'ksd':
         return main_ksd(args)
+    if args.workload == 'proxy':
+        return main_proxy(args)
 
     import torch
     import torch.distributed as dist
@@ -473,6 +476,103 @@ def main_ksd(args):
                          'kernel': f'ksd_colsum_kernel<{d},{str(gf).lower()}>', 'kernel_avg_us': round(colsum_s * 1e6, 1),
                          'flop_per_pair': flop_per_pair},
         }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_proxy(args):
+    """Proxy producers (stein_thinning.proxy; csrc/proxy.hip): log q and grad log q of config 5's
+    Gaussian proxy N(sample mean, 1.2 sample cov) -- or a Student-t proxy with the same shape,
+    df = 4 (--proxy-kind t) -- at every row of the n = 5e5, d = 50 sample, inputs resident in HBM.
+    N > 1: each rank evaluates its contiguous row block (no exchange)."""
+    import torch
+    import torch.distributed as dist
+    from stein_thinning import _native as nat
+    from stein_thinning import proxy
+    from stein_thinning.distributed import shard_bounds
+    rank, world, dev = _setup_ranks()
+    if world > 1:
+        _init_group(dev)
+    cfg = CONFIGS['c5']
+    x, _, _, _ = gaussian_d50(cfg['n'], cfg['seed'])
+    n, d = x.shape
+    mean = np.mean(x, axis=0)
+    cov = 1.2 * np.cov(x, rowvar=False)
+    t_kind = args.proxy_kind == 't'
+    df = 4.0 if t_kind else 0.0
+    psd = proxy._psd(cov, allow_singular=t_kind)
+    if t_kind:
+        from scipy.special import gammaln
+        c_log = float(gammaln(0.5 * (df + d)) - gammaln(0.5 * df) - d / 2. * np.log(df * np.pi) - 0.5 * psd.log_pdet)
+    else:
+        c_log = psd.rank * proxy._LOG_2PI + psd.log_pdet
+    r0, r1 = shard_bounds(n, rank, world)
+    rows = r1 - r0
+    xd = torch.from_numpy(np.ascontiguousarray(x[r0:r1])).to(dev)
+    loc = torch.from_numpy(mean).to(dev)
+    U = torch.from_numpy(np.ascontiguousarray(psd.U)).to(dev)
+    P = torch.from_numpy(np.ascontiguousarray(np.linalg.inv(cov))).to(dev)
+    lq = torch.empty(rows, dtype=torch.float64, device=dev)
+    gq = torch.empty((rows, d), dtype=torch.float64, device=dev)
+    L = nat.lib()
+
+    def run_once():
+        nat.check(L.st_proxy_logpdf_grad(nat.ptr(xd), rows, d, nat.ptr(loc), nat.ptr(U), nat.ptr(P), df, c_log,
+                                         nat.ptr(lq), nat.ptr(gq), nat.stream_handle()), 'st_proxy_logpdf_grad')
+    for _ in range(args.warmup):
+        run_once()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        run_once()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_s = float(np.mean([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
+    if world > 1:
+        dist.barrier()
+        elapsed, kern_s = _max_over_ranks([elapsed, kern_s], dev)
+    if rank == 0:
+        flop_row = 4 * d * d + 2 * d + (2 * d + 12 if t_kind else 2)
+        bytes_row = 16 * d + 8
+        tflops = rows * flop_row / kern_s / 1e12
+        gbs = rows * bytes_row / kern_s / 1e9
+        line = {
+            'metric': 'proxy rows/s (log q + grad log q per sample row)', 'value': n * args.steps / elapsed,
+            'unit': 'rows/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'strong',
+            'vs_baseline': None, 'dtype': 'f64', 'data': 'synthetic (config 5: iid N(0, AR(1) 0.5), d = 50)',
+            'config': {'workload': f"config 5 proxy: {'Student-t df=4' if t_kind else 'Gaussian'} "
+                                   'N(mean, 1.2 cov), n=5e5 d=50', 'n': n, 'd': d,
+                       'parallelism': f'row blocks x{world}' if world > 1 else 'single-gpu'},
+            'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
+                         'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': None,
+                         'kernel': 'proxy_kernel', 'kernel_avg_us': round(kern_s * 1e6, 1),
+                         'flop_per_row': flop_row, 'bytes_per_row': bytes_row,
+                         'hbm_view': {'achieved_GBs': round(gbs, 1), 'peak_GBs': HBM_PEAK_GBS,
+                                      'frac': round(gbs / HBM_PEAK_GBS, 4)}},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import proxy_numpy as op
+            m = 100_000
+            c0 = time.perf_counter()
+            if t_kind:
+                op.student_t_proxy(x[:m], mean, cov, df)
+            else:
+                op.gaussian_proxy(x[:m], mean, cov)
+            dt = time.perf_counter() - c0
+            line['cpu_baseline'] = {'value': m / dt, 'unit': 'rows/s', 'kind': 'reference',
+                                    'cores': int(os.environ.get('OMP_NUM_THREADS', os.cpu_count())),
+                                    'sample': f'scipy {"multivariate_t" if t_kind else "multivariate_normal"}.logpdf + '
+                                              f'the reference\'s einsum gradient on the first {m} rows ({dt:.2f} s; '
+                                              'BLAS threads as configured on the host)'}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

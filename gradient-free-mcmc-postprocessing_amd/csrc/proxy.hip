@@ -30,21 +30,45 @@ constexpr int kRows = 64;
 constexpr int kPitch = kRows + 1;
 constexpr int kThreads = 256;
 
+// Stage the (rows, d) row-major tile at xb into LDS as dev[r][k] = x - loc at s[r * rs + k * ks]:
+// CH coalesced loads per thread are issued before any is consumed (one wait per batch, not one per
+// element).
+template <int CH>
+__device__ inline void stage_tile(const double* __restrict__ xb, int rows, int d, const double* s_loc,
+                                  double* s, int rs, int ks) {
+    const int total = rows * d;
+    for (int base = 0; base < total; base += kThreads * CH) {
+        double v[CH];
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int e = base + threadIdx.x + kThreads * i;
+            v[i] = e < total ? xb[e] : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < CH; ++i) {
+            const int e = base + threadIdx.x + kThreads * i;
+            if (e < total) {
+                const int r = e / d;
+                const int k = e - r * d;
+                s[r * rs + k * ks] = v[i] - s_loc[k];
+            }
+        }
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void proxy_kernel(ProxyArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     const int d = a.d;
     double* s_dev = lds;                   // [d][kPitch]
     double* s_y = lds + d * kPitch;        // [d][kPitch]
     double* s_part = s_y + d * kPitch;     // [4][kRows]
+    double* s_loc = s_part + 4 * kRows;    // [d]
     const int64_t r0 = (int64_t)blockIdx.x * kRows;
     const int rows = (int)min<int64_t>(kRows, a.n - r0);
     const int tid = threadIdx.x;
-    const double* xb = a.x + r0 * d;
-    for (int e = tid; e < kRows * d; e += kThreads) {
-        const int r = e / d;
-        const int k = e - r * d;
-        s_dev[k * kPitch + r] = r < rows ? xb[e] - a.loc[k] : 0.0;
-    }
+    for (int k = tid; k < d; k += kThreads) s_loc[k] = a.loc[k];
+    __syncthreads();
+    stage_tile<8>(a.x + r0 * d, rows, d, s_loc, s_dev, 1, kPitch);   // rows >= `rows`: unused garbage
     __syncthreads();
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int lane = tid & 63;
@@ -112,12 +136,226 @@ __global__ __launch_bounds__(kThreads) void proxy_kernel(ProxyArgs a) {
     }
 }
 
+// ---- 16 < d <= 64: the two (64, d) x (d, d) products of a row tile on the matrix cores ---------
+// v_mfma_f64_16x16x4_f64 (gfx950 maps, cdna_hip_programming.md: A[l&15][k=l>>4], B[k=l>>4][l&15],
+// D col = l&15, row = (l>>4) + 4 reg).  Output columns: T = 2 ceil(d/16) tiles of 16 (z = dev @ U
+// tiles, then y = dev @ P^T tiles), wave w owns tiles w and w + 4; its B fragments (all k-steps)
+// stay in VGPRs for the life of the block, which loops over 64-row tiles (persistent grid).  Per
+// tile: the x tile is staged (coalesced) into LDS as dev = x - loc, each wave runs S = ceil(d/4)
+// k-steps x 4 row subtiles x its tiles of MFMAs, z^2 is reduced across the 16 column lanes, y goes
+// back through LDS and out as contiguous grad rows.
+constexpr int kMfmaMaxD = 64;
+constexpr int kMfmaMaxS = kMfmaMaxD / 4;
+typedef double dbl4 __attribute__((ext_vector_type(4)));
+
+// sum over the 16 lanes of a DPP row (every lane gets the total): quad xor 1, quad xor 2, half-row
+// mirror, row mirror -- VALU data movement instead of LDS permutes
+template <int CTRL>
+__device__ inline double dpp_f64(double v) {
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
+}
+__device__ inline double row16_sum(double v) {
+    v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
+    v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
+    v += dpp_f64<0x141>(v);   // row_half_mirror
+    v += dpp_f64<0x140>(v);   // row_mirror
+    return v;
+}
+
+__host__ __device__ inline int mfma_pitch(int dk) { return ((dk + 27) / 32) * 32 + 4; }   // = 4 mod 32 doubles
+
+__global__ __launch_bounds__(kThreads, 2) void proxy_mfma_kernel(ProxyArgs a) {
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int d = a.d;
+    const int S = (d + 3) / 4;
+    const int dk = 4 * S;
+    const int PD = mfma_pitch(dk);
+    const int PY = d + 1;
+    const int tz = (d + 15) / 16;            // z tiles (= y tiles)
+    double* s_dev = lds;                      // [64][PD]
+    double* s_y = s_dev + kRows * PD;         // [64][PY]
+    double* s_part = s_y + kRows * PY;        // [4][64]
+    double* s_coef = s_part + 4 * kRows;      // [64]
+    double* s_loc = s_coef + kRows;           // [d]
+    const int tid = threadIdx.x;
+    for (int k = tid; k < d; k += kThreads) s_loc[k] = a.loc[k];
+    for (int e = tid; e < kRows * (dk - d); e += kThreads) {   // k-padding columns: zero for good
+        const int r = e / (dk - d);
+        s_dev[r * PD + d + (e - r * (dk - d))] = 0.0;
+    }
+    const int lane = tid & 63;
+    const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int li = lane & 15, lk = lane >> 4;
+    // owned tiles: t0 = w, t1 = w + 4 (tile t < tz: z tile t; else y tile t - tz)
+    const int T = 2 * tz;
+    const bool has0 = w < T, has1 = w + 4 < T;
+    double b0[kMfmaMaxS], b1[kMfmaMaxS];
+    auto bval = [&](int t, int s) -> double {
+        const int k = 4 * s + lk;
+        if (t < tz) {
+            const int j = 16 * t + li;
+            return (k < d && j < d) ? a.U[(int64_t)k * d + j] : 0.0;
+        }
+        const int j = 16 * (t - tz) + li;
+        return (k < d && j < d) ? a.P[(int64_t)j * d + k] : 0.0;
+    };
+#pragma unroll
+    for (int s = 0; s < kMfmaMaxS; ++s) {
+        b0[s] = (has0 && s < S) ? bval(w, s) : 0.0;
+        b1[s] = (has1 && s < S) ? bval(w + 4, s) : 0.0;
+    }
+    const float inv_d = 1.0f / (float)d;
+    const int64_t ntiles = (a.n + kRows - 1) / kRows;
+    constexpr int kPf = kRows * kMfmaMaxD / kThreads;   // 16 prefetched doubles per thread
+    double pf[kPf];
+    auto prefetch = [&](int64_t tile) {   // issue the loads of a tile's x rows (consumed later)
+        const int64_t r0 = tile * kRows;
+        const int total = (int)min<int64_t>(kRows, a.n - r0) * d;
+        const double* xb = a.x + r0 * d;
+#pragma unroll
+        for (int i = 0; i < kPf; ++i) {
+            const int e = tid + kThreads * i;
+            pf[i] = e < total ? xb[e] : 0.0;
+        }
+    };
+    if (blockIdx.x < ntiles) prefetch(blockIdx.x);
+    for (int64_t tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+        const int64_t r0 = tile * kRows;
+        const int rows = (int)min<int64_t>(kRows, a.n - r0);
+        __syncthreads();   // s_loc / padding (first tile); the previous tile's readers are done
+#pragma unroll
+        for (int i = 0; i < kPf; ++i) {
+            const int e = tid + kThreads * i;
+            if (e < rows * d) {
+                const int r = (int)(((float)e + 0.5f) * inv_d);   // exact: e < 4096, d <= 64
+                const int k = e - r * d;
+                s_dev[r * PD + k] = pf[i] - s_loc[k];
+            }
+        }
+        __syncthreads();
+        if (tile + gridDim.x < ntiles) prefetch(tile + gridDim.x);   // overlaps this tile's MFMAs
+        // two passes of 32 rows (2 row subtiles each) keep the accumulators at 16 doubles
+#pragma unroll 1
+        for (int half = 0; half < 2; ++half) {
+            dbl4 acc0[2], acc1[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) { acc0[u] = dbl4{0, 0, 0, 0}; acc1[u] = dbl4{0, 0, 0, 0}; }
+#pragma unroll
+            for (int s = 0; s < kMfmaMaxS; ++s) {
+                if (s < S) {
+                    double av[2];
+#pragma unroll
+                    for (int u = 0; u < 2; ++u) av[u] = s_dev[(16 * (2 * half + u) + li) * PD + 4 * s + lk];
+                    if (has0) {
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) acc0[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], b0[s], acc0[u], 0, 0, 0);
+                    }
+                    if (has1) {
+#pragma unroll
+                        for (int u = 0; u < 2; ++u) acc1[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], b1[s], acc1[u], 0, 0, 0);
+                    }
+                }
+            }
+            // epilogue: z tiles -> per-row partial |z|^2 of this wave; y tiles -> s_y
+            double part[2][4];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) part[u][r] = 0.0;
+            auto take = [&](int t, dbl4* acc) {
+                if (t < tz) {
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int r = 0; r < 4; ++r) part[u][r] = fma(acc[u][r], acc[u][r], part[u][r]);
+                } else {
+                    const int j = 16 * (t - tz) + li;
+                    if (j < d) {
+#pragma unroll
+                        for (int u = 0; u < 2; ++u)
+#pragma unroll
+                            for (int r = 0; r < 4; ++r) s_y[(16 * (2 * half + u) + lk + 4 * r) * PY + j] = acc[u][r];
+                    }
+                }
+            };
+            if (has0) take(w, acc0);
+            if (has1) take(w + 4, acc1);
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const double v = row16_sum(part[u][r]);
+                    if (li == 0) s_part[w * kRows + 16 * (2 * half + u) + lk + 4 * r] = v;
+                }
+        }
+        __syncthreads();
+        if (w == 0) {
+            const double maha = ((s_part[lane] + s_part[kRows + lane]) + s_part[2 * kRows + lane]) +
+                                s_part[3 * kRows + lane];
+            double lq, coef;
+            if (a.df > 0.0) {
+                double my = 0.0;
+                for (int k = 0; k < d; ++k) my = fma(s_dev[lane * PD + k], s_y[lane * PY + k], my);
+                const double t = 0.5 * (a.df + (double)d);
+                lq = a.c_log + -t * log(1.0 + (1.0 / a.df) * maha);
+                coef = (-(a.df + (double)d) / a.df) / (1.0 + my / a.df);
+            } else {
+                lq = -0.5 * (a.c_log + maha);
+                coef = -1.0;
+            }
+            if (lane < rows) a.log_q[r0 + lane] = lq;
+            s_coef[lane] = coef;
+        }
+        __syncthreads();
+        double* gb = a.grad + r0 * d;
+        for (int base = 0; base < rows * d; base += 4 * kThreads) {   // LDS reads batched, then stores
+            double y[4], c[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = min(base + tid + kThreads * i, rows * d - 1);
+                const int r = (int)(((float)e + 0.5f) * inv_d);
+                y[i] = s_y[r * PY + (e - r * d)];
+                c[i] = s_coef[r];
+            }
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const int e = base + tid + kThreads * i;
+                if (e < rows * d) gb[e] = c[i] == -1.0 ? -y[i] : c[i] * y[i];
+            }
+        }
+    }
+}
+
 }  // namespace
 
-int64_t proxy_lds_bytes(int d) { return ((int64_t)2 * d * kPitch + 4 * kRows) * 8; }
+int64_t proxy_lds_bytes(int d) { return ((int64_t)2 * d * kPitch + 4 * kRows + d) * 8; }
+
+static int64_t proxy_mfma_lds_bytes(int d) {
+    const int dk = 4 * ((d + 3) / 4);
+    return ((int64_t)kRows * mfma_pitch(dk) + (int64_t)kRows * (d + 1) + 5 * kRows + d) * 8;
+}
+
+int g_proxy_mode = 0;   // 0: auto (matrix cores for 16 < d <= 64), 1: force the VALU kernel
 
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
+    if (g_proxy_mode == 0 && a.d > 16 && a.d <= kMfmaMaxD) {
+        const int64_t lds = proxy_mfma_lds_bytes(a.d);   // <= 69 KB at d = 64
+        static bool s_set = false;
+        if (!s_set) {
+            const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(proxy_mfma_kernel),
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+            if (e != hipSuccess) return e;
+            s_set = true;
+        }
+        const int64_t tiles = (a.n + kRows - 1) / kRows;
+        const int64_t grid = tiles < 2 * 256 ? tiles : 2 * 256;
+        proxy_mfma_kernel<<<dim3((unsigned)grid), kThreads, (size_t)lds, s>>>(a);
+        return hipGetLastError();
+    }
     const int64_t lds = proxy_lds_bytes(a.d);
     static int64_t s_lds_set = 0;   // raise the dynamic-LDS ceiling once (up to 130 KB at d = 128)
     if (lds > 65536 && lds > s_lds_set) {

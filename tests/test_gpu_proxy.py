@@ -32,7 +32,7 @@ def _case(n, d, seed):
     return x, mean, cov
 
 
-@pytest.mark.parametrize('d', [1, 2, 3, 4, 7, 8, 16, 50, 65, 128])
+@pytest.mark.parametrize('d', [1, 2, 3, 4, 7, 8, 16, 17, 32, 33, 50, 64, 65, 128])
 @pytest.mark.parametrize('n', [1, 63, 64, 65, 5000])
 def test_gaussian_proxy_matches_scipy(n, d):
     x, mean, cov = _case(n, d, 10 * d + n)
@@ -43,7 +43,7 @@ def test_gaussian_proxy_matches_scipy(n, d):
     _close(gq, wg)
 
 
-@pytest.mark.parametrize('d', [1, 2, 4, 9, 50, 128])
+@pytest.mark.parametrize('d', [1, 2, 4, 9, 20, 50, 64, 128])
 @pytest.mark.parametrize('df', [1.0, 3.0, 4.0, 30.5])
 def test_student_t_proxy_matches_scipy_and_notebook_gradient(d, df):
     x, loc, shape = _case(777, d, d + int(df * 10))
