@@ -222,7 +222,7 @@ def main():
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
-    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy'],
+    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
                          '(row-sharded, RCCL all-reduce of the n-length column-sum vector)')
     args = ap.parse_args()
@@ -230,6 +230,8 @@ def main():
         return main_ksd(args)
     if args.workload == 'proxy':
         return main_proxy(args)
+    if args.workload == 'lv':
+        return main_lv(args)
 
     import torch
     import torch.distributed as dist
@@ -573,6 +575,89 @@ def main_proxy(args):
                                     'sample': f'scipy {"multivariate_t" if t_kind else "multivariate_normal"}.logpdf + '
                                               f'the reference\'s einsum gradient on the first {m} rows ({dt:.2f} s; '
                                               'BLAS threads as configured on the host)'}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def main_lv(args):
+    """Lotka-Volterra gradients (stein_thinning.lotka_volterra; csrc/lv.hip): grad log posterior
+    from the forward sensitivity equations (RK45, scipy's algorithm) at 113 143 parameter points --
+    the unique-sample count of the reference's Dask/AWS gradient run -- drawn around the
+    data-generating theta.  N > 1: each rank evaluates a contiguous block of points."""
+    import torch
+    import torch.distributed as dist
+    from stein_thinning import _native as nat
+    from stein_thinning import lotka_volterra as lv
+    from stein_thinning.distributed import shard_bounds
+    rank, world, dev = _setup_ranks()
+    if world > 1:
+        _init_group(dev)
+    n = 113_143
+    rng = np.random.default_rng(12350)
+    theta = np.exp(np.log(lv.THETA) + 0.05 * rng.normal(size=(n, 4)))
+    data = lv.reference_data()
+    t, y, s = lv._settings(data, lv.RTOL, lv.ATOL)
+    cinv = np.ascontiguousarray(np.linalg.inv(data.cov))
+    r0, r1 = shard_bounds(n, rank, world)
+    m = r1 - r0
+    thd = torch.from_numpy(np.ascontiguousarray(theta[r0:r1])).to(dev)
+    td, yd = torch.from_numpy(t).to(dev), torch.from_numpy(y).to(dev)
+    out = torch.empty((m, 4), dtype=torch.float64, device=dev)
+    status = torch.zeros(m, dtype=torch.int32, device=dev)
+    L = nat.lib()
+
+    def run_once():
+        nat.check(L.st_lv_grad_log_posterior(nat.ptr(thd), m, nat.ptr(td), t.size, nat.ptr(yd), s.ctypes.data,
+                                             cinv.ctypes.data, lv.MAX_STEPS, nat.ptr(out), nat.ptr(status),
+                                             nat.stream_handle()), 'st_lv_grad_log_posterior')
+    for _ in range(args.warmup):
+        run_once()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        run_once()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    kern_s = float(np.mean([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
+    failed = int((status != 0).sum().item())
+    if world > 1:
+        dist.barrier()
+        elapsed, kern_s = _max_over_ranks([elapsed, kern_s], dev)
+    if rank == 0:
+        line = {
+            'metric': 'LV grad-log-posterior points/s (forward sensitivities, RK45)', 'value': n * args.steps / elapsed,
+            'unit': 'points/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': elapsed / args.steps * 1e3, 'higher_is_better': True, 'scaling': 'strong',
+            'vs_baseline': None, 'dtype': 'f64',
+            'data': 'synthetic parameter points exp(N(log theta*, 0.05^2)); observations = the reference module\'s data',
+            'config': {'workload': 'LV gradients at 113 143 points (Dask_AWS unique-sample count), t_n = 2400, '
+                                   'rtol 1e-3 / atol 1e-6', 'n': n,
+                       'parallelism': f'point blocks x{world}' if world > 1 else 'single-gpu'},
+            'roofline': {'bound': 'latency', 'achieved': None, 'peak': None, 'unit': None, 'frac': None,
+                         'traffic': None, 'kernel': 'lv_kernel<10>', 'kernel_avg_us': round(kern_s * 1e6, 1),
+                         'note': 'one thread per point running a divergent adaptive integration (~32 accepted '
+                                 'steps + 2400 dense-output evaluations); 358 VGPRs -> one wave per SIMD; '
+                                 '113 143 points fill 1 768 waves = 1.7 waves per SIMD'},
+            'failed_points': failed,
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            from oracle import lv_numpy as ol
+            k = 200
+            c0 = time.perf_counter()
+            for row in theta[:k]:
+                ol.grad_log_posterior(row, data.t, data.y, data.cov)
+            dt = time.perf_counter() - c0
+            line['cpu_baseline'] = {'value': k / dt, 'unit': 'points/s', 'cores': 1, 'kind': 'port',
+                                    'sample': f'oracle.lv_numpy.grad_log_posterior (the notebook function on '
+                                              f'scipy solve_ivp) for the first {k} points, {dt:.2f} s, one process'}
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

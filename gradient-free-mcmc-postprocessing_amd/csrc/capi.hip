@@ -337,6 +337,71 @@ int st_proxy_logpdf_grad(const double* x, int64_t n, int32_t d, const double* lo
     return hip_check(st::launch_proxy(a, static_cast<hipStream_t>(stream)), "proxy launch");
 }
 
+static int lv_common(st::LvArgs& a, const double* theta, int64_t n, const double* t_eval, int32_t t_n,
+                     const double* y_obs, const double* span_u0_tol, int64_t max_steps, double* out,
+                     int32_t* status) {
+    if (n < 0) return fail(ST_ERR_INVALID, "n must be >= 0");
+    if (t_n < 1) return fail(ST_ERR_INVALID, "t_n must be >= 1");
+    if (!span_u0_tol) return fail(ST_ERR_INVALID, "NULL solver settings");
+    if (max_steps < 1) return fail(ST_ERR_INVALID, "max_steps must be >= 1");
+    if (n > 0 && (!theta || !t_eval || !y_obs || !out || !status)) return fail(ST_ERR_INVALID, "NULL pointer");
+    const double t0 = span_u0_tol[0], t1 = span_u0_tol[1];
+    if (!(t1 > t0)) return fail(ST_ERR_INVALID, "need t1 > t0 (forward integration)");
+    if (!(span_u0_tol[4] > 0) || !(span_u0_tol[5] > 0)) return fail(ST_ERR_INVALID, "rtol and atol must be > 0");
+    a.theta = theta;
+    a.n = n;
+    a.t_eval = t_eval;
+    a.t_n = t_n;
+    a.y_obs = y_obs;
+    a.t0 = t0;
+    a.t1 = t1;
+    a.u0[0] = span_u0_tol[2];
+    a.u0[1] = span_u0_tol[3];
+    a.rtol = span_u0_tol[4];
+    a.atol = span_u0_tol[5];
+    a.max_steps = max_steps;
+    a.out = out;
+    a.status = status;
+    return ST_OK;
+}
+
+int st_lv_grad_log_posterior(const double* theta, int64_t n, const double* t_eval, int32_t t_n,
+                             const double* y_obs, const double* span_u0_tol, const double* cov_inv,
+                             int64_t max_steps, double* grad_out, int32_t* status, void* stream) {
+    st::LvArgs a{};
+    int rc = lv_common(a, theta, n, t_eval, t_n, y_obs, span_u0_tol, max_steps, grad_out, status);
+    if (rc) return rc;
+    if (!cov_inv) return fail(ST_ERR_INVALID, "NULL cov_inv");
+    for (int q = 0; q < 4; ++q) a.cinv[q] = cov_inv[q];
+    if (n == 0) return ST_OK;
+    return hip_check(st::launch_lv(a, true, static_cast<hipStream_t>(stream)), "lv gradient launch");
+}
+
+int64_t st_lv_log_density_workspace_bytes(int64_t n, int32_t t_n) {
+    if (n < 0 || t_n < 1) return -1;
+    return n * (int64_t)t_n * 8;
+}
+
+int st_lv_log_target_density(const double* log_theta, const double* theta, int64_t n,
+                             const double* t_eval, int32_t t_n, const double* y_obs,
+                             const double* span_u0_tol, const double* whiten, double c_log,
+                             double norm_logc, int64_t max_steps, double* out, int32_t* status,
+                             void* workspace, int64_t workspace_bytes, void* stream) {
+    st::LvArgs a{};
+    int rc = lv_common(a, theta, n, t_eval, t_n, y_obs, span_u0_tol, max_steps, out, status);
+    if (rc) return rc;
+    if (!whiten) return fail(ST_ERR_INVALID, "NULL whiten");
+    if (n > 0 && (!log_theta || !workspace)) return fail(ST_ERR_INVALID, "NULL log_theta / workspace");
+    if (workspace_bytes < n * (int64_t)t_n * 8) return fail(ST_ERR_INVALID, "workspace too small");
+    for (int q = 0; q < 4; ++q) a.U[q] = whiten[q];
+    a.log_theta = log_theta;
+    a.c_log = c_log;
+    a.norm_logc = norm_logc;
+    a.work = static_cast<double*>(workspace);
+    if (n == 0) return ST_OK;
+    return hip_check(st::launch_lv(a, false, static_cast<hipStream_t>(stream)), "lv log density launch");
+}
+
 int st_greedy_finalize(const double* cands_in, int32_t nranks, int32_t d, uint32_t* idx_out,
                        int64_t t, void* stream) {
     if (!cands_in || !idx_out) return fail(ST_ERR_INVALID, "NULL pointer");

@@ -1,0 +1,296 @@
+// Lotka-Volterra posterior inputs for Stein thinning, batched over parameter points: the gradient
+// of the log posterior from the forward sensitivity equations, and the log target density.
+//
+// Reference (code/src/lotka_volterra.py; Sensitivity_analysis.ipynb cells 16, 40, 46):
+//   grad_log_posterior(theta) = sum_k J_k^T C^-1 (y_k - u(t_k)) - log(theta) / theta
+//     u, J = du/dtheta from solve_ivp(lotka_volterra_sensitivity, [0, 25], [1, 1, 0 x 8],
+//     dense_output=True).sol(t): RK45 (Dormand-Prince), rtol 1e-3, atol 1e-6 (scipy defaults)
+//   log_target_density(log_theta) = sum_k mvn.logpdf(y_k - u(t_k), 0, C) + sum_j norm.logpdf(log_theta_j)
+//     u from solve_ivp(lotka_volterra, ...) (the 2-state system: its own step sequence)
+// One thread integrates one parameter point with scipy's algorithm step for step: initial step
+// selection (common.select_initial_step), the accept / reject loop of RungeKutta._step_impl
+// (SAFETY 0.9, factors in [0.2, 10], error exponent -1/5, RMS error norm), the tableau as scipy
+// holds it (rk45_tableau.hpp, generated), and dense output y = h Q p(x) + y_old per accepted step
+// with OdeSolution's segment rule (t in (t_j, t_j+1] -> segment j).  The observation points are
+// consumed in time order while the integration proceeds, so no trajectory is stored; the gradient
+// sums over time points sequentially (np.sum(axis=0) of the (t_n, 4) terms).  Summation orders
+// inside the BLAS products scipy uses (np.dot of stages) are not reproducible bit for bit:
+// results agree with scipy to rounding as long as the step sequences coincide.
+#include <hip/hip_runtime.h>
+
+#include "rk45_tableau.hpp"
+#include "stein_internal.hpp"
+
+namespace st {
+namespace {
+
+constexpr int kLvThreads = 64;
+
+template <int NS>
+__device__ inline void lv_rhs(const double th[4], const double* y, double* f) {
+    const double th1 = th[0], th2 = th[1], th3 = th[2], th4 = th[3];
+    const double u1 = y[0], u2 = y[1];
+    f[0] = th1 * u1 - th2 * u1 * u2;
+    f[1] = th4 * u1 * u2 - th3 * u2;
+    if constexpr (NS == 10) {
+        const double w1 = y[2], w2 = y[3], w3 = y[4], w4 = y[5];
+        const double w5 = y[6], w6 = y[7], w7 = y[8], w8 = y[9];
+        f[2] = u1 + (th1 - th2 * u2) * w1 - th2 * u1 * w5;
+        f[3] = -u1 * u2 + (th1 - th2 * u2) * w2 - th2 * u1 * w6;
+        f[4] = (th1 - th2 * u2) * w3 - th2 * u1 * w7;
+        f[5] = (th1 - th2 * u2) * w4 - th2 * u1 * w8;
+        f[6] = th4 * u2 * w1 + (th4 * u1 - th3) * w5;
+        f[7] = th4 * u2 * w2 + (th4 * u1 - th3) * w6;
+        f[8] = -u2 + th4 * u2 * w3 + (th4 * u1 - th3) * w7;
+        f[9] = u1 * u2 + th4 * u2 * w4 + (th4 * u1 - th3) * w8;
+    }
+}
+
+// scipy common.norm: np.linalg.norm(x) / x.size ** 0.5
+template <int NS>
+__device__ inline double rms(const double* v) {
+    double s = 0.0;
+#pragma unroll
+    for (int i = 0; i < NS; ++i) s += v[i] * v[i];
+    return sqrt(s) / sqrt((double)NS);
+}
+
+// NS = 10: gradient of the log posterior -> out[4 i + j]; NS = 2: per-time log-likelihood terms ->
+// work[k n + i] (summed by lv_logdens_finish)
+template <int NS>
+__global__ __launch_bounds__(kLvThreads) void lv_kernel(LvArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * kLvThreads + threadIdx.x;
+    if (i >= a.n) return;
+    double th[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) th[j] = a.theta[4 * i + j];
+    const double rtol = a.rtol, atol = a.atol;
+    double y[NS], f[NS], K[rk45::kStages + 1][NS];
+#pragma unroll
+    for (int c = 0; c < NS; ++c) y[c] = c < 2 ? a.u0[c] : 0.0;
+    double t = a.t0;
+    const double t_bound = a.t1;
+    lv_rhs<NS>(th, y, f);
+    // ---- select_initial_step (order = error estimator order 4, max_step = inf, direction +1)
+    double h_abs;
+    {
+        const double interval = fabs(t_bound - t);
+        double sc[NS], v[NS];
+#pragma unroll
+        for (int c = 0; c < NS; ++c) sc[c] = atol + fabs(y[c]) * rtol;
+#pragma unroll
+        for (int c = 0; c < NS; ++c) v[c] = y[c] / sc[c];
+        const double d0 = rms<NS>(v);
+#pragma unroll
+        for (int c = 0; c < NS; ++c) v[c] = f[c] / sc[c];
+        const double d1 = rms<NS>(v);
+        double h0 = (d0 < 1e-5 || d1 < 1e-5) ? 1e-6 : 0.01 * d0 / d1;
+        h0 = fmin(h0, interval);
+        double y1[NS], f1[NS];
+#pragma unroll
+        for (int c = 0; c < NS; ++c) y1[c] = y[c] + h0 * 1.0 * f[c];
+        lv_rhs<NS>(th, y1, f1);
+#pragma unroll
+        for (int c = 0; c < NS; ++c) v[c] = (f1[c] - f[c]) / sc[c];
+        const double d2 = rms<NS>(v) / h0;
+        double h1;
+        if (d1 <= 1e-15 && d2 <= 1e-15) h1 = fmax(1e-6, h0 * 1e-3);
+        else h1 = pow(0.01 / fmax(d1, d2), 1.0 / (rk45::kOrder + 1));
+        h_abs = fmin(fmin(100 * h0, h1), interval);   // max_step = inf
+    }
+    int kk = 0;                       // next observation point
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    int32_t status = 0;
+    for (int64_t step = 0;; ++step) {
+        if (t == t_bound) break;      // OdeSolver.step: finished
+        if (step >= a.max_steps) { status = 2; break; }
+        const double min_step = 10 * fabs(nextafter(t, INFINITY) - t);
+        if (h_abs < min_step) h_abs = min_step;   // (h_abs > max_step = inf never)
+        bool rejected = false;
+        double t_new, h, y_new[NS], f_new[NS];
+        for (;;) {
+            if (h_abs < min_step) { status = 1; break; }
+            h = h_abs;
+            t_new = t + h;
+            if (t_new - t_bound > 0) t_new = t_bound;
+            h = t_new - t;
+            h_abs = fabs(h);
+            // rk_step
+#pragma unroll
+            for (int c = 0; c < NS; ++c) K[0][c] = f[c];
+#pragma unroll
+            for (int s = 1; s < rk45::kStages; ++s) {
+                double ys[NS];
+#pragma unroll
+                for (int c = 0; c < NS; ++c) {
+                    double dy = K[0][c] * rk45::A[s][0];
+#pragma unroll
+                    for (int j = 1; j < s; ++j) dy += K[j][c] * rk45::A[s][j];
+                    ys[c] = y[c] + dy * h;
+                }
+                lv_rhs<NS>(th, ys, K[s]);
+            }
+#pragma unroll
+            for (int c = 0; c < NS; ++c) {
+                double bsum = K[0][c] * rk45::B[0];
+#pragma unroll
+                for (int j = 1; j < rk45::kStages; ++j) bsum += K[j][c] * rk45::B[j];
+                y_new[c] = y[c] + h * bsum;
+            }
+            lv_rhs<NS>(th, y_new, f_new);
+#pragma unroll
+            for (int c = 0; c < NS; ++c) K[rk45::kStages][c] = f_new[c];
+            double ev[NS];
+#pragma unroll
+            for (int c = 0; c < NS; ++c) {
+                double e = K[0][c] * rk45::E[0];
+#pragma unroll
+                for (int j = 1; j <= rk45::kStages; ++j) e += K[j][c] * rk45::E[j];
+                const double scale = atol + fmax(fabs(y[c]), fabs(y_new[c])) * rtol;
+                ev[c] = e * h / scale;
+            }
+            const double error_norm = rms<NS>(ev);
+            if (error_norm < 1) {
+                double factor = error_norm == 0 ? rk45::kMaxFactor
+                                                : fmin(rk45::kMaxFactor, rk45::kSafety * pow(error_norm, rk45::kErrorExponent));
+                if (rejected) factor = fmin(1.0, factor);
+                h_abs *= factor;
+                break;
+            }
+            h_abs *= fmax(rk45::kMinFactor, rk45::kSafety * pow(error_norm, rk45::kErrorExponent));
+            rejected = true;
+        }
+        if (status) break;
+        // dense output of this step: Q = K^T P; points t in (t_old, t_new] (all remaining at the end)
+        double Q[NS][rk45::kDenseOrder];
+#pragma unroll
+        for (int c = 0; c < NS; ++c)
+#pragma unroll
+            for (int q = 0; q < rk45::kDenseOrder; ++q) {
+                double s = K[0][c] * rk45::P[0][q];
+#pragma unroll
+                for (int j = 1; j <= rk45::kStages; ++j) s += K[j][c] * rk45::P[j][q];
+                Q[c][q] = s;
+            }
+        const double t_old = t;
+        const double hd = t_new - t_old;
+        const bool last = t_new - t_bound >= 0;
+        while (kk < a.t_n && (last || a.t_eval[kk] <= t_new)) {
+            const double x = (a.t_eval[kk] - t_old) / hd;
+            const double p1 = x, p2 = p1 * x, p3 = p2 * x, p4 = p3 * x;
+            double u[NS];
+#pragma unroll
+            for (int c = 0; c < NS; ++c)
+                u[c] = hd * (((Q[c][0] * p1 + Q[c][1] * p2) + Q[c][2] * p3) + Q[c][3] * p4) + y[c];
+            const double r0 = a.y_obs[2 * kk] - u[0], r1 = a.y_obs[2 * kk + 1] - u[1];
+            if constexpr (NS == 10) {
+                const double g0 = a.cinv[0] * r0 + a.cinv[1] * r1;
+                const double g1 = a.cinv[2] * r0 + a.cinv[3] * r1;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) acc[j] += u[2 + j] * g0 + u[6 + j] * g1;
+            } else {
+                const double z0 = r0 * a.U[0] + r1 * a.U[2];
+                const double z1 = r0 * a.U[1] + r1 * a.U[3];
+                a.work[(int64_t)kk * a.n + i] = -0.5 * (a.c_log + (z0 * z0 + z1 * z1));
+            }
+            ++kk;
+        }
+        t = t_new;
+#pragma unroll
+        for (int c = 0; c < NS; ++c) { y[c] = y_new[c]; f[c] = f_new[c]; }
+    }
+    a.status[i] = status;
+    if constexpr (NS == 10) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            a.out[4 * i + j] = status ? NAN : acc[j] - log(th[j]) / th[j];
+    } else if (status) {
+        for (; kk < a.t_n; ++kk) a.work[(int64_t)kk * a.n + i] = NAN;
+    }
+}
+
+// numpy pairwise_sum (loops_utils.h.src, PW_BLOCKSIZE 128) over a strided column: the recursion
+// (sum(first n2) + sum(rest), n2 = n/2 rounded down to a multiple of 8, leaves <= 128) walked
+// post-order with an explicit stack
+__device__ inline double pairwise_leaf(const double* a, int64_t n, int64_t stride) {
+    if (n < 8) {
+        double res = -0.0;
+        for (int64_t k = 0; k < n; ++k) res += a[k * stride];
+        return res;
+    }
+    double r[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) r[q] = a[q * stride];
+    int64_t k;
+    for (k = 8; k < n - (n % 8); k += 8)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) r[q] += a[(k + q) * stride];
+    double res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    for (; k < n; ++k) res += a[k * stride];
+    return res;
+}
+
+__device__ double pairwise_sum_strided(const double* a, int64_t n, int64_t stride) {
+    struct Frame { int64_t off, cnt; int state; double left; };
+    Frame st[40];   // depth <= log2(n / 128) + 1
+    int sp = 0;
+    st[0] = {0, n, 0, 0.0};
+    double ret = 0.0;
+    while (sp >= 0) {
+        Frame& f = st[sp];
+        if (f.cnt <= 128) {
+            ret = pairwise_leaf(a + f.off * stride, f.cnt, stride);
+            --sp;
+            continue;
+        }
+        int64_t n2 = f.cnt / 2;
+        n2 -= n2 % 8;
+        if (f.state == 0) {
+            f.state = 1;
+            st[sp + 1] = {f.off, n2, 0, 0.0};
+            ++sp;
+        } else if (f.state == 1) {
+            f.left = ret;
+            f.state = 2;
+            st[sp + 1] = {f.off + n2, f.cnt - n2, 0, 0.0};
+            ++sp;
+        } else {
+            ret = f.left + ret;
+            --sp;
+        }
+    }
+    return ret;
+}
+
+// log_likelihood = np.sum(per-time terms) (0.0 + pairwise), log_prior = np.sum(norm.logpdf(log_theta))
+__global__ __launch_bounds__(kLvThreads) void lv_logdens_finish(LvArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * kLvThreads + threadIdx.x;
+    if (i >= a.n) return;
+    const double ll = 0.0 + pairwise_sum_strided(a.work + i, a.t_n, a.n);
+    double lp = -0.0;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const double x = a.log_theta[4 * i + j];
+        lp += -(x * x) / 2.0 - a.norm_logc;
+    }
+    lp = 0.0 + lp;
+    a.out[i] = ll + lp;
+}
+
+}  // namespace
+
+hipError_t launch_lv(const LvArgs& a, bool gradient, hipStream_t s) {
+    if (a.n <= 0) return hipSuccess;
+    const unsigned blocks = (unsigned)((a.n + kLvThreads - 1) / kLvThreads);
+    if (gradient) {
+        lv_kernel<10><<<blocks, kLvThreads, 0, s>>>(a);
+        return hipGetLastError();
+    }
+    lv_kernel<2><<<blocks, kLvThreads, 0, s>>>(a);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    lv_logdens_finish<<<blocks, kLvThreads, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+}  // namespace st

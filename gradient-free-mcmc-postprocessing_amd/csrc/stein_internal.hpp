@@ -89,6 +89,27 @@ struct ProxyArgs {
 int64_t proxy_lds_bytes(int d);
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s);
 
+struct LvArgs {
+    const double* theta;      // (n, 4) row-major ODE parameters
+    const double* log_theta;  // (n, 4) row-major, log density only
+    int64_t n;
+    const double* t_eval;     // (t_n) ascending observation times
+    int t_n;
+    const double* y_obs;      // (t_n, 2) row-major observations
+    double t0, t1;            // integration span
+    double u0[2];             // initial state
+    double rtol, atol;
+    double cinv[4];           // inv(C) row-major (gradient)
+    double U[4];              // scipy _PSD(C).U row-major (log density)
+    double c_log;             // rank * log(2 pi) + log_pdet of C
+    double norm_logc;         // scipy.stats.norm's log(sqrt(2 pi))
+    int64_t max_steps;
+    double* out;              // gradient: (n, 4); log density: (n)
+    double* work;             // log density: (t_n, n) per-time terms
+    int32_t* status;          // (n): 0 ok, 1 step size too small, 2 step limit reached
+};
+hipError_t launch_lv(const LvArgs& a, bool gradient, hipStream_t s);
+
 hipError_t launch_greedy_rank_exchange(const double* recs, int K, int64_t stride, int d,
                                        const MailboxPeers& peers, int rank, int nranks, int64_t t,
                                        double* recv, unsigned* status, hipStream_t s);

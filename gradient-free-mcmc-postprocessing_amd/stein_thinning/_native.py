@@ -73,6 +73,11 @@ SIGNATURES = {
     'st_greedy_step_exchange': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
                                                _i64, _i64, _i32, _i32, _c_dp, _c_dp, _c_dp, _c_dp,
                                                _c_dp, _i64, _c_dp, _c_dp]),
+    'st_lv_grad_log_posterior': (ctypes.c_int, [_c_dp, _i64, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _i64, _c_dp,
+                                                _c_dp, _c_dp]),
+    'st_lv_log_density_workspace_bytes': (_i64, [_i64, _i32]),
+    'st_lv_log_target_density': (ctypes.c_int, [_c_dp, _c_dp, _i64, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _f64,
+                                                _f64, _i64, _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
     'st_proxy_logpdf_grad': (ctypes.c_int, [_c_dp, _i64, _i32, _c_dp, _c_dp, _c_dp, _f64, _f64, _c_dp,
                                             _c_dp, _c_dp]),
 }

@@ -177,6 +177,31 @@ int st_proxy_logpdf_grad(const double *x, int64_t n, int32_t d, const double *lo
                          double *log_q_out, double *grad_out, void *stream);
 
 /* ------------------------------------------------------------------------------------------
+ * Lotka-Volterra inputs, batched over n parameter points (one RK45 integration per point, scipy's
+ * solve_ivp algorithm step for step -- code/src/lotka_volterra.py):
+ *   st_lv_grad_log_posterior: grad_out (n, 4) row-major = grad_log_posterior(theta) of
+ *     Sensitivity_analysis.ipynb cells 40, 46 (forward sensitivities, solve_ivp(
+ *     lotka_volterra_sensitivity, ..., dense_output=True).sol(t));
+ *   st_lv_log_target_density: out (n) = lotka_volterra.log_target_density(log_theta) (2-state
+ *     system), theta = exp(log_theta) computed by the caller (NumPy's exp, as the reference).
+ * theta, log_theta: (n, 4) row-major device arrays; t_eval (t_n) ascending and y_obs (t_n, 2)
+ * row-major: the observation times and data (device); span_u0_tol: HOST array {t0, t1, u0_1,
+ * u0_2, rtol, atol}; cov_inv: HOST (2, 2) row-major inv(C); whiten: HOST (2, 2) row-major scipy
+ * _PSD(C).U with c_log = rank * log(2 pi) + log_pdet; norm_logc = log(sqrt(2 pi)) (scipy.stats.norm).
+ * status (n, device): 0 ok, 1 step size fell below scipy's min_step (output NaN), 2 max_steps
+ * reached (output NaN).  Results agree with scipy to rounding (BLAS summation orders differ).
+ * ---------------------------------------------------------------------------------------- */
+int st_lv_grad_log_posterior(const double *theta, int64_t n, const double *t_eval, int32_t t_n,
+                             const double *y_obs, const double *span_u0_tol, const double *cov_inv,
+                             int64_t max_steps, double *grad_out, int32_t *status, void *stream);
+int64_t st_lv_log_density_workspace_bytes(int64_t n, int32_t t_n);
+int st_lv_log_target_density(const double *log_theta, const double *theta, int64_t n,
+                             const double *t_eval, int32_t t_n, const double *y_obs,
+                             const double *span_u0_tol, const double *whiten, double c_log,
+                             double norm_logc, int64_t max_steps, double *out, int32_t *status,
+                             void *workspace, int64_t workspace_bytes, void *stream);
+
+/* ------------------------------------------------------------------------------------------
  * Integrand protocol -- replaces integrand(ind1, ind2) of the closures returned by
  * stein_thinning.thinning._make_stein_integrand / _make_stein_gf_integrand and
  * stein_thinning.kernel.vfk0_imq (restated at JAX_Stein_Thinning.ipynb cell 27, json ~354-361;
