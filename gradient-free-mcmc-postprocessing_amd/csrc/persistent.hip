@@ -34,7 +34,7 @@ namespace {
 
 constexpr int kMaxPWaves = 8;                // up to 512-thread blocks
 constexpr int kShards = 8;
-constexpr int kMaxGrid = 256;               // one block per CU on MI355X (256 CUs)
+constexpr int kMaxGrid = 512;               // up to two blocks per CU on MI355X (256 CUs)
 constexpr int kMaxRanks = kMailboxRanks;    // GPUs of one node
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
 constexpr uint64_t kFirstRankTimeoutTicks = 1000000000ull;   // 10 s: peers' launch skew at step 0
@@ -169,8 +169,9 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 // the in-order vmcnt wait in front of the row's use.  After the wave MINLOC the winning lane
 // writes the row to sc->row.  Returns the winner's index, or -1 if the sweep timed out (grid-wide
 // abort).
-template <int D, bool GF>
+template <int D, bool GF, int MAXG>
 __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
+    static_assert(MAXG % 64 == 0 && MAXG <= kMaxGrid && MAXG / 64 <= 32, "records per lane");
     constexpr int kRow = 2 * D + (GF ? 1 : 0);
     const int G = gridDim.x;
     ST_STAMP(a, t + 1, 0);
@@ -181,7 +182,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t need = 0;
 #pragma unroll
-        for (int c = 0; c < kMaxGrid / 64; ++c) need |= (lane + 64 * c < G) ? (1u << c) : 0u;
+        for (int c = 0; c < MAXG / 64; ++c) need |= (lane + 64 * c < G) ? (1u << c) : 0u;
         uint32_t seen = 0;
         double v = INFINITY;
         int64_t gi = INT64_MAX;
@@ -206,13 +207,13 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         for (;; ++it) {
             // all four loads unconditionally (records past G read as zeros: the descriptor's range
             // check), so they issue back to back and a poll costs ONE round trip, not four
-            u32x4 qs[kMaxGrid / 64];
+            u32x4 qs[MAXG / 64];
 #pragma unroll
-            for (int c = 0; c < kMaxGrid / 64; ++c)
+            for (int c = 0; c < MAXG / 64; ++c)
                 qs[c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (lane + 64 * c) * kRecGranules * 8,
                                                               0, 16 /* sc1 */);
 #pragma unroll
-            for (int c = 0; c < kMaxGrid / 64; ++c) {
+            for (int c = 0; c < MAXG / 64; ++c) {
                 if ((need & ~seen) & (1u << c)) {
                     const u32x4 q = qs[c];
                     const uint64_t g0 = ((uint64_t)q.y << 32) | q.x;
@@ -331,9 +332,13 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
     return sc->i[0];
 }
 
-template <int D, bool GF, int RT, int NT>
-__global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
+// BPC = blocks per CU: 2 puts two 256-thread blocks on each CU (two waves per SIMD, RT <= 8
+// register rows each, every block its own record): the fp64 pipe issues from two waves
+template <int D, bool GF, int RT, int NT, int BPC>
+__global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     constexpr int kPBlock = NT;
+    constexpr int kMaxG = 256 * BPC;     // records swept per step
+    constexpr bool kTwoWaves = NT >= 512 || BPC > 1;   // two waves per SIMD
     extern __shared__ __attribute__((aligned(16))) double lds[];
     Scratch* sc = reinterpret_cast<Scratch*>(lds);
     const int RL = a.RL;
@@ -423,7 +428,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
     int64_t t = 1;
     for (; t < a.m; ++t) {
-        const int64_t win = wait_and_pick<D, GF>(a, sc, t - 1);
+        const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, t - 1);
         if (win < 0) break;
         if (blockIdx.x == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
         double xj[D], gj[D];
@@ -458,7 +463,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
             };
             // (with two waves per SIMD the registers are too tight to carry the prefetched pair
             // through the on-chip rows: the 512-thread variant issues it after them)
-            constexpr bool kEarlyStream = NT <= 256;
+            constexpr bool kEarlyStream = !kTwoWaves;
             int64_t srow = str_base + tid;
             // opaque per step: otherwise LICM hoists the ~20 64-bit load addresses of the first
             // streamed pair out of the step loop and they end up spilled to scratch
@@ -480,7 +485,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
                 if (q == 0) { bv = ar[q]; bq = 0; } else scan_take_v<FAST>(ar[q], (uint32_t)q, bv, bq);
                 // two waves per SIMD hide latency by themselves: cap the scheduler's interleaving
                 // of independent rows (it costs registers the 512-thread variant does not have)
-                if constexpr (NT >= 512) {
+                if constexpr (kTwoWaves) {
                     if ((q & 1) == 1) __builtin_amdgcn_sched_barrier(0);
                 }
             }
@@ -503,7 +508,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
                 return av;
             };
             // (two waves per SIMD: two chains per wave are enough and leave room for the rows)
-            constexpr int UL = NT >= 512 ? 2 : 4;
+            constexpr int UL = kTwoWaves ? 2 : 4;
             int e = tid;
             for (; e + (UL - 1) * kPBlock < RL; e += UL * kPBlock) {
                 double av[UL];
@@ -521,8 +526,18 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
                 if constexpr (GF) kv = (kv * r.w) * wj;
                 return add_twice<FAST>(r.a, kv);
             };
-            if (!kEarlyStream && srow < r1) { fetch(srow, c0); fetch(srow + kPBlock, c1); }
-            while (srow < r1) {
+            if constexpr (kTwoWaves) {
+                // two waves per SIMD: one row at a time, no prefetch registers (the other wave
+                // computes while this one waits for its loads)
+                for (; srow < r1; srow += kPBlock) {
+                    SRow r;
+                    fetch(srow, r);
+                    const double av = stream_pair(r);
+                    a.A[srow] = av;
+                    scan_take_v<FAST>(av, (uint32_t)srow, bv, bi);
+                }
+            }
+            while (!kTwoWaves && srow < r1) {
                 const int64_t nrow = srow + 2 * kPBlock;
                 SRow n0, n1;
                 fetch(nrow, n0);
@@ -549,7 +564,7 @@ __global__ __launch_bounds__(NT, 1) void greedy_persistent(PersistArgs a) {
     }
     int64_t done = t;   // idx[0 .. done-1) are written
     if (t == a.m) {
-        const int64_t win = wait_and_pick<D, GF>(a, sc, a.m - 1);
+        const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, a.m - 1);
         if (win >= 0) {
             if (blockIdx.x == 0 && tid == 0) a.idx_out[a.m - 1] = (uint32_t)win;
             done = a.m + 1;
@@ -583,6 +598,7 @@ int64_t persistent_ws_bytes(int d, int G) {
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
 static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (256)
 static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (one per CU)
+static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
 static uint64_t* g_stamps = nullptr;
 #ifdef ST_PERSIST_STAMPS
 extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
@@ -603,12 +619,17 @@ int persistent_tune(int key, int value) {
         g_persist_grid = value;
         return 0;
     }
+    if (key == 8) {
+        if (value != -1 && value != 1 && value != 2) return -1;
+        g_persist_bpc = value;
+        return 0;
+    }
     return -1;
 }
 
-template <int D, bool GF, int RT, int NT>
+template <int D, bool GF, int RT, int NT, int BPC = 1>
 static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s) {
-    auto fn = greedy_persistent<D, GF, RT, NT>;
+    auto fn = greedy_persistent<D, GF, RT, NT, BPC>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -625,7 +646,11 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
 }
 
 template <int D, bool GF>
-static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int G, size_t lds, hipStream_t s) {
+static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int G, size_t lds, hipStream_t s) {
+    if (bpc == 2) {
+        if (rt <= 4) return launch_p<D, GF, 4, 256, 2>(a, G, lds, s);
+        return launch_p<D, GF, 8, 256, 2>(a, G, lds, s);
+    }
     if (nt == 512) {
         if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s);
         if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s);
@@ -666,24 +691,25 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         lds_optin > lds_max)
         lds_max = lds_optin;
     if (lds_max > 163840) lds_max = 163840;
-    int G = cus > kMaxGrid ? kMaxGrid : cus;
+    const int nt = g_persist_nt > 0 ? g_persist_nt : 256;
+    const int bpc = (nt == 256 && g_persist_bpc == 2) ? 2 : 1;
+    int G = cus * bpc > kMaxGrid ? kMaxGrid : cus * bpc;
     if (g_persist_grid > 0 && G > g_persist_grid) G = g_persist_grid;
     const int64_t min_rows = 256;   // fewer blocks for small n: exchange cost grows with G
     if (n_shard < (int64_t)G * min_rows) G = (int)((n_shard + min_rows - 1) / min_rows);
     if (G < 1) G = 1;
     if (persistent_ws_bytes(d, G) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n_shard + G - 1) / G;
-    const int nt = g_persist_nt > 0 ? g_persist_nt : 256;
-    const int rt_max = nt == 512 ? 8 : 16;
+    const int rt_max = (nt == 512 || bpc == 2) ? 8 : 16;
     int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
     if (rt != 4 && rt != 6 && rt != 8 && rt != 16) rt = rt_max;
     if (rt > rt_max) rt = rt_max;
-    if (rt == 6 && nt != 512) rt = 8;
+    if (rt == 6 && (nt != 512 || bpc == 2)) rt = 8;
     while (rt > 4 && (int64_t)rt * nt > R) rt = rt == 6 ? 4 : rt / 2;   // no empty register rows
     const bool gf = w != nullptr;
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);
     const size_t head = (sizeof(Scratch) + 15) / 16 * 16;
-    const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) - 1024;   // static + slack
+    const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) / bpc - 1024;   // static + slack
     int64_t RL = (int64_t)((budget - head) / row_bytes);
     const int64_t need = R - (int64_t)rt * nt;
     if (RL > need) RL = need > 0 ? need : 0;
@@ -711,8 +737,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     // zero status and every granule tag (a stale tag from a previous run must never match)
     hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G), s);
     if (e != hipSuccess) return e;
-    if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, nt, G, lds, s) : launch_p_rt<2, false>(a, rt, nt, G, lds, s);
-    else e = gf ? launch_p_rt<4, true>(a, rt, nt, G, lds, s) : launch_p_rt<4, false>(a, rt, nt, G, lds, s);
+    if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s);
+    else e = gf ? launch_p_rt<4, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<4, false>(a, rt, nt, bpc, G, lds, s);
     if (e == hipSuccess) *used = 1;
     return e;
 }

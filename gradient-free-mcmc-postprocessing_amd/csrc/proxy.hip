@@ -338,7 +338,13 @@ static int64_t proxy_mfma_lds_bytes(int d) {
     return ((int64_t)kRows * mfma_pitch(dk) + (int64_t)kRows * (d + 1) + 5 * kRows + d) * 8;
 }
 
-int g_proxy_mode = 0;   // 0: auto (matrix cores for 16 < d <= 64), 1: force the VALU kernel
+static int g_proxy_mode = 0;   // 0: auto (matrix cores for 16 < d <= 64), 1: always the VALU kernel
+
+int proxy_tune(int value) {
+    if (value != 0 && value != 1) return -1;
+    g_proxy_mode = value;
+    return 0;
+}
 
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;

@@ -88,6 +88,7 @@ struct ProxyArgs {
 };
 int64_t proxy_lds_bytes(int d);
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s);
+int proxy_tune(int value);   // st_tune key 7
 
 struct LvArgs {
     const double* theta;      // (n, 4) row-major ODE parameters

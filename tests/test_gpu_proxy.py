@@ -90,3 +90,20 @@ def test_gaussian_thin_selects_the_reference_points_d50():
     got = proxy.gaussian_thin(x, log_p, mean, qcov, 60)
     want = op.gaussian_thin(x, log_p, mean, qcov, 60)
     np.testing.assert_array_equal(got, want)
+
+
+@pytest.mark.parametrize('d', [17, 50, 64])
+def test_valu_and_matrix_core_kernels_agree(d):
+    """The VALU kernel (st_tune key 7 = 1) on the d range the MFMA kernel serves by default."""
+    from stein_thinning import _native as nat
+    x, mean, cov = _case(3000, d, 99 + d)
+    wl, wg = op.gaussian_proxy(x, mean, cov)
+    lm, gm = proxy.gaussian_proxy(x, mean, cov)
+    assert nat.lib().st_tune(7, 1) == 0
+    try:
+        lv_, gv = proxy.gaussian_proxy(x, mean, cov)
+    finally:
+        nat.lib().st_tune(7, 0)
+    for lq, gq in ((lm, gm), (lv_, gv)):
+        _close(lq, wl)
+        _close(gq, wg)

@@ -186,7 +186,10 @@ int main(int argc, char** argv) {
     st_tune(4, -1);
 #ifdef ST_PERSIST_STAMPS
     {   // phase breakdown of persistent steps 20..51 (s_memrealtime, 10 ns ticks)
-        const int SP = 32, PH = 10, GMAX = 256;
+        const int SP = 32, PH = 10, GMAX = 512;
+        if (getenv("PROBE_BPC")) st_tune(8, atoi(getenv("PROBE_BPC")));
+        if (getenv("PROBE_NT")) st_tune(4, atoi(getenv("PROBE_NT")));
+        if (getenv("PROBE_RT")) st_tune(3, atoi(getenv("PROBE_RT")));
         uint64_t* dst;
         CK(hipMalloc(&dst, sizeof(uint64_t) * GMAX * SP * PH));
         CK(hipMemset(dst, 0, sizeof(uint64_t) * GMAX * SP * PH));
