@@ -174,6 +174,39 @@ def test_persistent_and_fallback_bit_exact(tune):
     assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
 
 
+@pytest.mark.parametrize('knobs', [
+    ('two blocks per CU, 8 register rows', {8: 2}),
+    ('two blocks per CU, 4 register rows', {8: 2, 3: 4}),
+    ('512-thread blocks, 8 register rows', {4: 512, 3: 8}),
+    ('512-thread blocks, 6 register rows', {4: 512, 3: 6}),
+])
+@pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
+def test_persistent_two_wave_variants_bit_exact(knobs, d, gf):
+    """The optional two-waves-per-SIMD persistent variants (st_tune keys 3, 4, 8) against the C
+    model: identical indices, bit-identical running sums."""
+    from stein_thinning import _native
+    n, m = 700_001, 20
+    x, g = _rw_chain(n, d, seed=11 + d)
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    w = None
+    if gf:
+        lw = -0.2 * np.sum(x * x, axis=1)
+        w = np.exp(lw - lw.min())
+    L = _native.lib()
+    for k, v in knobs[1].items():
+        assert L.st_tune(k, v) == 0
+    try:
+        idx, A = DeviceProblem(s, gs, w, l, tr).greedy(m, return_sums=True)
+    finally:
+        for k in (3, 4, 8):
+            L.st_tune(k, -1)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    np.testing.assert_array_equal(idx, cidx)
+    assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
+
+
 @pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
 def test_persistent_exact_path_outside_fast_range(d, gf):
     """Rows with components outside [2^-60, 2^60] (tiny / huge scores, tiny coordinates) force the
