@@ -117,12 +117,12 @@ def log_target_density(log_theta, data: Optional[LvData] = None, rtol: float = R
     """``lotka_volterra.log_target_density`` for every row of ``log_theta`` ((n, 4) or (4,)):
     returns (n,)."""
     import torch
-    from scipy.stats._multivariate import _PSD
+    from .proxy import PsdFactor
     data = reference_data() if data is None else data
     lth = _points(log_theta)
     th = np.exp(lth)                                   # as the reference: np.exp(log_theta)
     t, y, s = _settings(data, rtol, atol)
-    psd = _PSD(np.asarray(data.cov, dtype=np.float64), allow_singular=False)
+    psd = PsdFactor(np.asarray(data.cov, dtype=np.float64), allow_singular=False)
     c_log = psd.rank * float(np.log(2 * np.pi)) + psd.log_pdet
     U = np.ascontiguousarray(psd.U, dtype=np.float64)
     norm_logc = float(np.log(np.sqrt(2 * np.pi)))      # scipy.stats._continuous_distns._norm_pdf_logC

@@ -29,9 +29,32 @@ from . import _native as nat
 _LOG_2PI = float(np.log(2 * np.pi))   # scipy.stats._multivariate._LOG_2PI
 
 
-def _psd(m: np.ndarray, allow_singular: bool):
-    from scipy.stats._multivariate import _PSD   # the factorisation scipy's logpdf uses
-    return _PSD(m, allow_singular=allow_singular)
+class PsdFactor:
+    """The factorisation scipy's multivariate_normal / multivariate_t logpdf use
+    (scipy.stats._multivariate._PSD, restated on its public pieces so the same doubles come out):
+    eigh of the lower triangle, eigenvalues below 1e6 * eps * max|eigenvalue| treated as zero,
+    U = eigenvectors * sqrt(pseudo-inverse eigenvalues) (so U U^T = pinv(M)), log pseudo-determinant
+    and rank."""
+
+    def __init__(self, m: np.ndarray, allow_singular: bool = True):
+        import scipy.linalg
+        m = np.asarray(m)
+        s, u = scipy.linalg.eigh(m, lower=True, check_finite=True)
+        eps = 1e6 * np.finfo(s.dtype.char.lower()).eps * np.max(abs(s))
+        if np.min(s) < -eps:
+            raise ValueError('The input matrix must be symmetric positive semidefinite.')
+        d = s[s > eps]
+        if len(d) < len(s) and not allow_singular:
+            raise np.linalg.LinAlgError('When `allow_singular is False`, the input matrix must be '
+                                        'symmetric positive definite.')
+        s_pinv = np.array([0 if abs(x) <= eps else 1 / x for x in s], dtype=float)
+        self.U = np.multiply(u, np.sqrt(s_pinv))
+        self.rank = len(d)
+        self.log_pdet = np.sum(np.log(d))
+
+
+def _psd(m: np.ndarray, allow_singular: bool) -> PsdFactor:
+    return PsdFactor(m, allow_singular=allow_singular)
 
 
 def _params(sample, loc, cov):

@@ -66,3 +66,21 @@ def test_product_validates_arguments_before_any_device_work():
         proxy.student_t_proxy(x, np.zeros(3), np.eye(3), 0.0)
     with pytest.raises(ValueError, match='df'):
         proxy.student_t_proxy(x, np.zeros(3), np.eye(3), np.inf)
+
+
+@pytest.mark.parametrize('d', [1, 2, 5, 50])
+def test_psd_factor_is_scipys(d):
+    """stein_thinning.proxy.PsdFactor returns scipy's _PSD factor bit for bit (the kernel's U)."""
+    from scipy.stats._multivariate import _PSD
+    from stein_thinning.proxy import PsdFactor
+    rng = np.random.default_rng(d)
+    m = _spd(d, rng)
+    for allow in (True, False):
+        a, b = PsdFactor(m, allow), _PSD(m, allow_singular=allow)
+        assert np.array_equal(a.U, b.U) and a.rank == b.rank and a.log_pdet == b.log_pdet
+    sing = np.diag([1.0] * (d - 1) + [0.0]) if d > 1 else np.zeros((1, 1))
+    with pytest.raises(np.linalg.LinAlgError):
+        PsdFactor(sing, allow_singular=False)
+    if d > 1:
+        a, b = PsdFactor(sing, True), _PSD(sing, allow_singular=True)
+        assert np.array_equal(a.U, b.U) and a.rank == b.rank
