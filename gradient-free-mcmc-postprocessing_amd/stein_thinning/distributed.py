@@ -243,12 +243,7 @@ class PeerMailboxes:
 
     def _agree(self, flag: bool) -> bool:
         """Group-wide AND of a per-rank flag."""
-        import torch
-        import torch.distributed as dist
-        dev = self.device if dist.get_backend(self.group) == 'nccl' else torch.device('cpu')
-        t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=self.group)
-        return bool(int(t.item()))
+        return _group_all(flag, self.group)
 
     def handshake(self) -> bool:
         """Every rank stores a token into every peer's mailbox and polls its own (device side,
@@ -283,6 +278,31 @@ class PeerMailboxes:
         self.ok = False
 
 
+def _group_all(flag: bool, group=None) -> bool:
+    """Group-wide AND of a per-rank flag (RCCL on the device under nccl, host tensor under gloo)."""
+    import torch
+    import torch.distributed as dist
+    dev = nat.require_device() if dist.get_backend(group) == 'nccl' else torch.device('cpu')
+    t = torch.tensor([1 if flag else 0], dtype=torch.int32, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+def _group_same(idx: np.ndarray, group=None) -> bool:
+    """True iff every rank holds the same index vector (min and max of a 63-bit digest agree)."""
+    import hashlib
+
+    import torch
+    import torch.distributed as dist
+    h = int.from_bytes(hashlib.sha256(np.ascontiguousarray(idx).tobytes()).digest()[:8], 'little') >> 1
+    dev = nat.require_device() if dist.get_backend(group) == 'nccl' else torch.device('cpu')
+    lo = torch.tensor([h], dtype=torch.int64, device=dev)
+    hi = lo.clone()
+    dist.all_reduce(lo, op=dist.ReduceOp.MIN, group=group)
+    dist.all_reduce(hi, op=dist.ReduceOp.MAX, group=group)
+    return int(lo.item()) == int(hi.item())
+
+
 _MAILBOXES = {}
 
 
@@ -299,9 +319,13 @@ def peer_mailboxes(group=None) -> PeerMailboxes:
 def exchange_engine(d: int, world: int) -> str:
     """Engine of a ``world``-rank run at dimension d: 'persistent' (d = 2, 4: one persistent launch
     per rank, winners exchanged in-kernel), 'steps' (other d: launch-per-step kernels in a HIP graph,
-    records exchanged by a mailbox kernel), or 'rccl' (RCCL all-gather per step; forced by
-    ST_SHARDED_EXCHANGE=rccl, and the fallback when the mailboxes cannot be set up)."""
-    if not 2 <= world <= MAX_PEER_RANKS or os.environ.get('ST_SHARDED_EXCHANGE', 'device') == 'rccl':
+    records exchanged by a mailbox kernel), 'replicated' (d = 2, 4, ST_SHARDED_EXCHANGE=replicated:
+    every GPU thins the whole sample; also the d = 2, 4 fallback) or 'rccl' (RCCL all-gather per
+    step; forced by ST_SHARDED_EXCHANGE=rccl, and the fallback otherwise)."""
+    choice = os.environ.get('ST_SHARDED_EXCHANGE', 'device')
+    if choice == 'replicated' and d in (2, 4):
+        return 'replicated'
+    if not 2 <= world <= MAX_PEER_RANKS or choice == 'rccl':
         return 'rccl'
     return 'persistent' if d in (2, 4) else 'steps'
 
@@ -340,6 +364,39 @@ class PersistentShardedGreedy:
             self.rank, self.world, self.mb.table_ptr(), seq, self.n_points, nat.ptr(self.idx),
             nat.ptr(self.a), nat.ptr(self.ws), self.ws.numel() * 8, nat.stream_handle()),
             'st_greedy_sharded')
+
+    def indices(self) -> np.ndarray:
+        return self.idx.cpu().numpy().view(np.uint32).copy()
+
+    def completed(self, idx: Optional[np.ndarray] = None) -> bool:
+        idx = self.indices() if idx is None else idx
+        return bool(idx.size == 0 or int(idx.max()) < self.prob.n)
+
+    def run(self) -> np.ndarray:
+        self.launch()
+        return self.indices()
+
+
+class ReplicatedGreedy:
+    """Every rank runs the WHOLE greedy thin on its own GPU (the single-device persistent kernel
+    over the replicated arrays): no exchange, and identical indices on every rank (same inputs,
+    same deterministic kernel; checked on the first run).  The fallback for d = 2, 4 when the
+    device exchange cannot be used: one GPU's time per thin, against ~25 us per step for an RCCL
+    all-gather of per-step records at these sizes."""
+
+    mode = 'replicated'
+
+    def __init__(self, integrand: SteinIntegrand, n_points: int, problem=None):
+        from .device import DeviceProblem
+        self.device = nat.require_device()
+        self.prob = problem if problem is not None else DeviceProblem(
+            integrand.sample, integrand.gradient, integrand.weights, integrand.linv_scale,
+            integrand.linv_trace, self.device)
+        self.n_points = int(n_points)
+        self.idx, self.a, self.ws = self.prob.greedy_buffers(self.n_points)
+
+    def launch(self) -> None:
+        self.prob.greedy_launch(self.n_points, self.idx, self.a, self.ws)
 
     def indices(self) -> np.ndarray:
         return self.idx.cpu().numpy().view(np.uint32).copy()
@@ -482,14 +539,24 @@ class _EagerRecords:
 def sharded_runner(integrand: SteinIntegrand, n_points: int, group=None, use_graph: bool = True):
     """Collective: build this rank's runner for a row-sharded greedy run and complete one run with
     it (the validation run; its result is ``runner.indices()``).  Tries the device-exchange engine
-    (exchange_engine) first; if any rank's bounded wait expired, every rank falls back to RCCL.
-    ``runner.mode`` names the engine; ``runner.launch()`` enqueues a further run."""
+    (exchange_engine) first; if the mailboxes cannot be set up or any rank's bounded wait expired,
+    every rank falls back together: for d = 2, 4 to the replicated run (each GPU thins the whole
+    sample; indices compared across ranks), otherwise -- or if that disagrees -- to the RCCL
+    record all-gather.  ``runner.mode`` names the engine; ``runner.launch()`` enqueues a further
+    run."""
     import torch.distributed as dist
     rank, world = _world(group)
     d = integrand.sample.shape[1]
     engine = exchange_engine(d, world)
     note = ''
-    if engine != 'rccl':
+    if engine == 'replicated':
+        runner = ReplicatedGreedy(integrand, n_points)
+        runner.launch()
+        idx = runner.indices()
+        if _group_all(runner.completed(idx), group) and _group_same(idx, group):
+            return runner
+        note = 'replicated runs disagree; '
+    elif engine != 'rccl':
         mb = peer_mailboxes(group)
         if mb.ok:
             if engine == 'persistent':
@@ -504,11 +571,19 @@ def sharded_runner(integrand: SteinIntegrand, n_points: int, group=None, use_gra
                 ok = backend.exchange_ok()
             if mb._agree(ok):
                 return runner
-            mb.ok = False   # a bounded wait expired somewhere: RCCL path from now on
+            mb.ok = False   # a bounded wait expired somewhere: no device exchange from now on
             mb.error = f'{engine} device exchange timed out'
             note = 'device exchange timed out; '
         else:
             note = f'device exchange unavailable ({mb.error}); '
+        if engine == 'persistent':
+            runner = ReplicatedGreedy(integrand, n_points)
+            runner.launch()
+            idx = runner.indices()
+            if _group_all(runner.completed(idx), group) and _group_same(idx, group):
+                runner.mode = note + 'replicated'
+                return runner
+            note += 'replicated runs disagree; '
     r0, r1 = shard_bounds(integrand.n, rank, world)
     backend = HipShardBackend(integrand, r0, r1, world, n_points)
     if dist.is_initialized() and dist.get_backend(group) == 'nccl':

@@ -102,6 +102,17 @@ def test_step_device_exchange_processes_share_one_gpu(tmp_path, world, gf, d):
             np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
 
 
+def test_replicated_engine_processes_share_one_gpu(tmp_path):
+    """ST_SHARDED_EXCHANGE=replicated (also the d = 2, 4 fallback when the device exchange is
+    unavailable): every rank thins the whole sample with the single-GPU kernel, indices agree."""
+    mp.spawn(_worker, args=(2, _free_port(), 'gloo', False, str(tmp_path), 'replicated', 2), nprocs=2, join=True)
+    for run in range(2):
+        want = _want(run % 2 == 1)
+        for r in range(2):
+            assert (tmp_path / f'mode{r}_{run}.txt').read_text() == 'replicated'
+            np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
+
+
 def test_single_rank_rccl_graph_capture(tmp_path):
     mp.spawn(_worker, args=(1, _free_port(), 'nccl', False, str(tmp_path)), nprocs=1, join=True)
     x, g, _, _ = _data()
