@@ -290,7 +290,7 @@ def main():
 
     roofline = None
     cpu = None
-    persistent = d in (2, 4) and (not sharded or runner.mode == 'device-exchange')
+    persistent = (d in (2, 4) and not sharded) or (sharded and runner.mode == 'device-exchange')
     if rank == 0 or sharded:
         gf = integrand.weights is not None
         bytes_per_pair = 16 * d + (24 if gf else 16)

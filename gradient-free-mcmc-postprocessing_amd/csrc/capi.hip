@@ -254,7 +254,8 @@ int st_greedy_sharded(const double* x_soa, const double* g_soa, const double* we
         workspace_bytes, static_cast<hipStream_t>(stream), &used, &rs);
     if (used) return ST_OK;
     if (e == hipErrorNotSupported)
-        return fail(ST_ERR_UNSUPPORTED, "multi-rank persistent kernel: d = %d not supported (d = 2, 4)", d);
+        return fail(ST_ERR_UNSUPPORTED, "multi-rank persistent kernel: d = %d not supported (d = 2, 4; d = 50 "
+                    "with at most 256 rows per CU)", d);
     (void)hipGetLastError();
     return hip_check(e, "multi-rank persistent launch");
 }

@@ -38,16 +38,21 @@ constexpr int kMaxGrid = 512;               // up to two blocks per CU on MI355X
 constexpr int kMaxRanks = kMailboxRanks;    // GPUs of one node
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
 constexpr uint64_t kFirstRankTimeoutTicks = 1000000000ull;   // 10 s: peers' launch skew at step 0
+// wide variant (D > 8, instantiated for D = 50): one row per thread in registers and no LDS or
+// streamed rows -- only when a block's rows fit (R <= 256: shards up to 256 x #CU rows, e.g. one
+// rank of an 8-GPU config-5 run); the winner row is read from LDS inside the pair loop
+constexpr int kWideD = 50;
 
 __device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minloc(v, i); }
 
 struct Scratch {          // small per-block scratch at the start of the dynamic LDS region
-    double row[2 * kMaxCtDim + 2];
+    double row[2 * kWideD + 2];   // winner row {x[d], g[d], w}
     double vblk;          // this block's last published minimum (NaN iff some row's A is NaN)
     double v[kMaxPWaves];
     int64_t i[kMaxPWaves];
     int abort;
-    int pad[3];
+    int rowfast;          // wide d: the winner row lies in the fast range (set by the fetching wave)
+    int pad[2];
 };
 
 // Per-thread argmin scan: every thread visits its rows in increasing index order, so a candidate
@@ -78,6 +83,56 @@ __device__ __forceinline__ double uniform(double v) {
     const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)b);
     const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(b >> 32));
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+// Wide d: pair_value_ct's arithmetic (same operations, same order -> same bits) for a row whose x
+// is in registers and whose g is in LDS (gi[k * gs]) against the winner row in LDS, eight
+// coordinates per stage with a scheduling barrier between stages, so LDS values are read just
+// before use instead of being hoisted into VGPRs next to the register row.
+template <int D, bool FAST>
+__device__ __forceinline__ double pair_value_wide(const double (&xi)[D], const double* gi, int gs,
+                                                  const double* xj, const double* gj, double l,
+                                                  double l2, double tr) {
+    static_assert(D >= 8, "wide variant");
+    constexpr int full = D - (D % 8);
+    double qs = 0.0, t1s = 0.0, t2s = 0.0, t3s = 0.0;
+    double r[8];
+#pragma unroll
+    for (int k0 = 0; k0 < D; k0 += 8) {
+        double bx[8], bg[8], ag[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j)
+            if (k0 + j < D) { bx[j] = xj[k0 + j]; bg[j] = gj[k0 + j]; ag[j] = gi[(k0 + j) * gs]; }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int k = k0 + j;
+            if (k < D) {
+                const double dl = xi[k] - bx[j];
+                const double gd = ag[j] - bg[j];
+                const double q = (l * dl) * dl;
+                const double u = (l2 * dl) * dl;
+                const double v = (l * gd) * dl;
+                if (k == 0) {
+                    qs = q; t1s = u; t2s = v;
+                } else {
+                    qs = qs + q; t1s = t1s + u; t2s = t2s + v;
+                }
+                const double p = ag[j] * bg[j];
+                if (k < 8) {
+                    r[k] = p;
+                } else if (k < full) {
+                    r[k % 8] += p;
+                } else {
+                    if (k == full) t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+                    t3s += p;
+                }
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    }
+    if constexpr (full == D) t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+    if constexpr (FAST) return finish_pair_fast(qs, t1s, t2s, t3s, tr);
+    else return finish_pair(qs, t1s, t2s, t3s, tr);
 }
 
 }  // namespace
@@ -172,7 +227,10 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 template <int D, bool GF, int MAXG>
 __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
     static_assert(MAXG % 64 == 0 && MAXG <= kMaxGrid && MAXG / 64 <= 32, "records per lane");
-    constexpr int kRow = 2 * D + (GF ? 1 : 0);
+    constexpr bool kWide = D > kMaxCtDim;
+    // wide rows are not prefetched into registers (2d + 1 doubles per lane): the wave loads the
+    // winner's row into LDS after the pick
+    constexpr int kRow = kWide ? 1 : 2 * D + (GF ? 1 : 0);
     const int G = gridDim.x;
     ST_STAMP(a, t + 1, 0);
     if (threadIdx.x < 64) {
@@ -191,12 +249,16 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
 #pragma unroll
         for (int k = 0; k < kRow; ++k) rowv[k] = 0.0;
         auto load_row = [&](int64_t r) {
+            if constexpr (kWide) {
+                (void)r;
+            } else {
 #pragma unroll
-            for (int k = 0; k < D; ++k) {
-                rowv[k] = a.x[(int64_t)k * a.ld + r];
-                rowv[D + k] = a.g[(int64_t)k * a.ld + r];
+                for (int k = 0; k < D; ++k) {
+                    rowv[k] = a.x[(int64_t)k * a.ld + r];
+                    rowv[D + k] = a.g[(int64_t)k * a.ld + r];
+                }
+                if constexpr (GF) rowv[2 * D] = a.w[r];
             }
-            if constexpr (GF) rowv[2 * D] = a.w[r];
         };
         int ok_all = 1;
         unsigned it = 0;
@@ -316,9 +378,25 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                 a.stamps[((int64_t)blockIdx.x * kStampSteps + (t + 1 - kStampFirst)) * kStampPhases + 8] =
                     row_of != gi ? 2 : 1;
 #endif
-            if (row_of != gi) load_row(gi);
+            if constexpr (!kWide) {
+                if (row_of != gi) load_row(gi);
 #pragma unroll
-            for (int k = 0; k < kRow; ++k) sc->row[k] = rowv[k];
+                for (int k = 0; k < kRow; ++k) sc->row[k] = rowv[k];
+            }
+        }
+        if constexpr (kWide) {   // the winner is wave-uniform now: 64 lanes fetch its 2d (+1) values
+            int fast = 1;
+            if (ok_all && gi != INT64_MAX) {
+                constexpr int kWRow = 2 * D + (GF ? 1 : 0);
+                for (int k = lane; k < kWRow; k += 64) {
+                    const double v = k < D ? a.x[(int64_t)k * a.ld + gi]
+                                           : (k < 2 * D ? a.g[(int64_t)(k - D) * a.ld + gi] : a.w[gi]);
+                    sc->row[k] = v;
+                    if (k < 2 * D) fast &= fast_range_ok(v);
+                }
+            }
+            fast = __all(fast);
+            if (lane == 0) sc->rowfast = fast;
         }
         if (lane == 0) {
             if (!ok_all) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -339,6 +417,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     constexpr int kPBlock = NT;
     constexpr int kMaxG = 256 * BPC;     // records swept per step
     constexpr bool kTwoWaves = NT >= 512 || BPC > 1;   // two waves per SIMD
+    constexpr bool kWide = D > kMaxCtDim;              // register rows only (host guarantees it)
     extern __shared__ __attribute__((aligned(16))) double lds[];
     Scratch* sc = reinterpret_cast<Scratch*>(lds);
     const int RL = a.RL;
@@ -357,7 +436,9 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     // ---- stage the block's rows on chip ----------------------------------------------------
     // and decide whether every row of the block admits the range-guarded fast pair arithmetic
     // (stein_math.hpp fast_range_ok; padding rows are zeros)
-    double xr[RT > 0 ? RT : 1][D], gr[RT > 0 ? RT : 1][D], ar[RT > 0 ? RT : 1];
+    // wide d: x in registers, g in LDS (sgw[k][NT], where the LDS rows would start: RL = 0)
+    double xr[RT > 0 ? RT : 1][D], gr[RT > 0 ? RT : 1][kWide ? 1 : D], ar[RT > 0 ? RT : 1];
+    double* sgw = sx;
     double wr[(GF && RT > 0) ? RT : 1];
     int rok = fast_range_ok(l) & (int)(l > 0.0) & (int)(tr > 0.0) & (int)(tr <= 0x1p64);
 #pragma unroll
@@ -367,26 +448,30 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
 #pragma unroll
         for (int k = 0; k < D; ++k) {
             xr[q][k] = ok ? a.x[k * ld + row] : 0.0;
-            gr[q][k] = ok ? a.g[k * ld + row] : 0.0;
-            rok &= fast_range_ok(xr[q][k]) & fast_range_ok(gr[q][k]);
+            const double gv = ok ? a.g[k * ld + row] : 0.0;
+            if constexpr (kWide) sgw[k * kPBlock + tid] = gv;
+            else gr[q][k] = gv;
+            rok &= fast_range_ok(xr[q][k]) & fast_range_ok(gv);
         }
         if constexpr (GF) wr[q] = ok ? a.w[row] : 0.0;
     }
-    for (int e = tid; e < RL; e += kPBlock) {
-        const int64_t row = lds_base + e;
-        const bool ok = row < r1;
+    if constexpr (!kWide) {
+        for (int e = tid; e < RL; e += kPBlock) {
+            const int64_t row = lds_base + e;
+            const bool ok = row < r1;
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-            const double xv = ok ? a.x[k * ld + row] : 0.0, gv = ok ? a.g[k * ld + row] : 0.0;
-            sx[k * RL + e] = xv;
-            sg[k * RL + e] = gv;
-            rok &= fast_range_ok(xv) & fast_range_ok(gv);
+            for (int k = 0; k < D; ++k) {
+                const double xv = ok ? a.x[k * ld + row] : 0.0, gv = ok ? a.g[k * ld + row] : 0.0;
+                sx[k * RL + e] = xv;
+                sg[k * RL + e] = gv;
+                rok &= fast_range_ok(xv) & fast_range_ok(gv);
+            }
+            if constexpr (GF) sw[e] = ok ? a.w[row] : 0.0;
         }
-        if constexpr (GF) sw[e] = ok ? a.w[row] : 0.0;
-    }
-    for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
+        for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
 #pragma unroll
-        for (int k = 0; k < D; ++k) rok &= fast_range_ok(a.x[k * ld + row]) & fast_range_ok(a.g[k * ld + row]);
+            for (int k = 0; k < D; ++k) rok &= fast_range_ok(a.x[k * ld + row]) & fast_range_ok(a.g[k * ld + row]);
+        }
     }
     const int block_fast = __syncthreads_and(rok);
 
@@ -398,30 +483,40 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
 #pragma unroll
     for (int q = 0; q < RT; ++q) {
         const int64_t row = r0 + (int64_t)q * kPBlock + tid;
-        double kv = diag_value_ct<D>(gr[q], tr);
+        double kv;
+        if constexpr (kWide) {
+            double gt[D];
+#pragma unroll
+            for (int k = 0; k < D; ++k) gt[k] = sgw[k * kPBlock + tid];
+            kv = diag_value_ct<D>(gt, tr);
+        } else {
+            kv = diag_value_ct<D>(gr[q], tr);
+        }
         if constexpr (GF) kv = (kv * wr[q]) * wr[q];
         ar[q] = row < r1 ? kv : INFINITY;   // padding rows hold +inf for the whole run
         if (q == 0) { bv = ar[q]; bi = (uint32_t)row; } else scan_take(ar[q], (uint32_t)row, bv, bi);
     }
-    for (int e = tid; e < RL; e += kPBlock) {
-        const int64_t row = lds_base + e;
-        double gi[D];
+    if constexpr (!kWide) {
+        for (int e = tid; e < RL; e += kPBlock) {
+            const int64_t row = lds_base + e;
+            double gi[D];
 #pragma unroll
-        for (int k = 0; k < D; ++k) gi[k] = sg[k * RL + e];
-        double kv = diag_value_ct<D>(gi, tr);
-        if constexpr (GF) kv = (kv * sw[e]) * sw[e];
-        kv = row < r1 ? kv : INFINITY;
-        sa[e] = kv;
-        scan_take(kv, (uint32_t)row, bv, bi);
-    }
-    for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
-        double gi[D];
+            for (int k = 0; k < D; ++k) gi[k] = sg[k * RL + e];
+            double kv = diag_value_ct<D>(gi, tr);
+            if constexpr (GF) kv = (kv * sw[e]) * sw[e];
+            kv = row < r1 ? kv : INFINITY;
+            sa[e] = kv;
+            scan_take(kv, (uint32_t)row, bv, bi);
+        }
+        for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
+            double gi[D];
 #pragma unroll
-        for (int k = 0; k < D; ++k) gi[k] = a.g[k * ld + row];
-        double kv = diag_value_ct<D>(gi, tr);
-        if constexpr (GF) kv = (kv * a.w[row]) * a.w[row];
-        a.A[row] = kv;
-        scan_take(kv, (uint32_t)row, bv, bi);
+            for (int k = 0; k < D; ++k) gi[k] = a.g[k * ld + row];
+            double kv = diag_value_ct<D>(gi, tr);
+            if constexpr (GF) kv = (kv * a.w[row]) * a.w[row];
+            a.A[row] = kv;
+            scan_take(kv, (uint32_t)row, bv, bi);
+        }
     }
     publish<NT>(a, sc, bv, bi, 0, r1);
 
@@ -431,17 +526,24 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
         const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, t - 1);
         if (win < 0) break;
         if (blockIdx.x == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
-        double xj[D], gj[D];
+        // small d: the winner row in SGPRs (VALU fp64 ops take one scalar operand); wide d: read
+        // from LDS inside the pair loop (block-uniform broadcast reads)
+        double xj_r[kWide ? 1 : D], gj_r[kWide ? 1 : D];
+        const double* xj = kWide ? sc->row : xj_r;
+        const double* gj = kWide ? sc->row + D : gj_r;
         // fast variant: range-guarded arithmetic (block rows and winner row in range) and a
         // NaN-free scan -- valid while no A of this block is NaN: the block's last minimum is NaN
         // iff one is, and fast steps keep finite sums finite (|2k| < 2^191 per step)
         int wfast = (block_fast != 0) & (int)!__builtin_isnan(sc->vblk);
+        if constexpr (kWide) {
+            wfast &= sc->rowfast;   // checked by the wave that fetched the row (no 2d reloads here)
+        } else {
 #pragma unroll
-        for (int k = 0; k < D; ++k) {
-            // block-uniform: keep the winner row in SGPRs (VALU fp64 ops take one scalar operand)
-            xj[k] = uniform(sc->row[k]);
-            gj[k] = uniform(sc->row[D + k]);
-            wfast &= fast_range_ok(xj[k]) & fast_range_ok(gj[k]);
+            for (int k = 0; k < D; ++k) {
+                xj_r[k] = uniform(sc->row[k]);
+                gj_r[k] = uniform(sc->row[D + k]);
+                wfast &= fast_range_ok(xj[k]) & fast_range_ok(gj[k]);
+            }
         }
         const double wj = GF ? uniform(sc->row[2 * D]) : 1.0;
         // one block-uniform choice per step: range-guarded fast arithmetic or the general one
@@ -450,6 +552,20 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             // opaque marker: keeps LLVM from if-converting the two variants into
             // compute-both-and-select (both are pure arithmetic over the register rows)
             asm volatile(";; sweep_rows variant" ::);
+            if constexpr (kWide) {   // register rows only (x in VGPRs, g in LDS)
+                uint32_t bq = 0;
+#pragma unroll
+                for (int q = 0; q < RT; ++q) {
+                    const int64_t row = r0 + (int64_t)q * kPBlock + tid;
+                    double kv = pair_value_wide<D, FAST>(xr[q], sgw + tid, kPBlock, xj, gj, l, l2, tr);
+                    if constexpr (GF) kv = (kv * wr[q]) * wj;
+                    if constexpr (FAST) ar[q] = add_twice<true>(ar[q], kv);
+                    else ar[q] = row < r1 ? add_twice<false>(ar[q], kv) : INFINITY;
+                    if (q == 0) { bv = ar[q]; bq = 0; } else scan_take_v<FAST>(ar[q], (uint32_t)q, bv, bq);
+                }
+                bi = (uint32_t)(r0 + tid) + bq * (uint32_t)kPBlock;
+                ST_STAMP_AFTER(a, t, 5, bv);
+            } else {
             // streamed rows go two at a time; the first pair's loads are issued now and land while
             // the on-chip rows compute.  Addresses of rows past r1 are clamped to r0 (a valid row
             // of this block): their loads are harmless and their results are dropped.
@@ -553,6 +669,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                 c1 = n1;
                 srow = nrow;
             }
+            }   // !kWide
         };
         // the flag is block-uniform (same LDS row, same block flag): make that explicit so the
         // branch is scalar and the two variants stay separate code paths
@@ -672,7 +789,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     const RankSpec one{0, n, 0, 1, 0, nullptr, {}};
     if (!rs) rs = &one;
     // 32-bit row indices, padding rows included (< n + one block's register rows)
-    if (g_persist_rt == 0 || (d != 2 && d != 4) || m < 1 || m >= 0xFFFFFFFFll || n >= 0x7FFFFFFFll)
+    const bool wide = d == kWideD;
+    if (g_persist_rt == 0 || (d != 2 && d != 4 && !wide) || m < 1 || m >= 0xFFFFFFFFll || n >= 0x7FFFFFFFll)
         return hipErrorNotSupported;
     if (rs->nranks < 1 || rs->nranks > kMaxRanks || rs->rank < 0 || rs->rank >= rs->nranks ||
         rs->row_begin < 0 || rs->row_end <= rs->row_begin || rs->row_end > n ||
@@ -691,8 +809,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         lds_optin > lds_max)
         lds_max = lds_optin;
     if (lds_max > 163840) lds_max = 163840;
-    const int nt = g_persist_nt > 0 ? g_persist_nt : 256;
-    const int bpc = (nt == 256 && g_persist_bpc == 2) ? 2 : 1;
+    const int nt = wide ? 256 : (g_persist_nt > 0 ? g_persist_nt : 256);
+    const int bpc = (!wide && nt == 256 && g_persist_bpc == 2) ? 2 : 1;
     int G = cus * bpc > kMaxGrid ? kMaxGrid : cus * bpc;
     if (g_persist_grid > 0 && G > g_persist_grid) G = g_persist_grid;
     const int64_t min_rows = 256;   // fewer blocks for small n: exchange cost grows with G
@@ -700,12 +818,14 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     if (G < 1) G = 1;
     if (persistent_ws_bytes(d, G) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n_shard + G - 1) / G;
+    if (wide && R > 256) return hipErrorNotSupported;   // wide: one register row per thread only
     const int rt_max = (nt == 512 || bpc == 2) ? 8 : 16;
     int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
     if (rt != 4 && rt != 6 && rt != 8 && rt != 16) rt = rt_max;
     if (rt > rt_max) rt = rt_max;
     if (rt == 6 && (nt != 512 || bpc == 2)) rt = 8;
     while (rt > 4 && (int64_t)rt * nt > R) rt = rt == 6 ? 4 : rt / 2;   // no empty register rows
+    if (wide) rt = 1;
     const bool gf = w != nullptr;
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);
     const size_t head = (sizeof(Scratch) + 15) / 16 * 16;
@@ -715,7 +835,10 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     if (RL > need) RL = need > 0 ? need : 0;
     RL = RL / 64 * 64;
     if (RL < 0) RL = 0;
-    const size_t lds = head + (size_t)RL * row_bytes;
+    if (wide) RL = 0;
+    // wide: the rows' g lives in LDS (d x 256 doubles: 100 KB at d = 50)
+    const size_t lds = wide ? head + (size_t)d * 256 * sizeof(double) : head + (size_t)RL * row_bytes;
+    if (wide && lds > (size_t)(lds_max > 0 ? lds_max : 65536)) return hipErrorNotSupported;
 
     char* p = static_cast<char*>(ws);
     PersistArgs a{};
@@ -737,7 +860,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     // zero status and every granule tag (a stale tag from a previous run must never match)
     hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G), s);
     if (e != hipSuccess) return e;
-    if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s);
+    if (wide) e = gf ? launch_p<kWideD, true, 1, 256>(a, G, lds, s) : launch_p<kWideD, false, 1, 256>(a, G, lds, s);
+    else if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s);
     else e = gf ? launch_p_rt<4, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<4, false>(a, rt, nt, bpc, G, lds, s);
     if (e == hipSuccess) *used = 1;
     return e;

@@ -316,10 +316,22 @@ def peer_mailboxes(group=None) -> PeerMailboxes:
     return mb
 
 
-def exchange_engine(d: int, world: int) -> str:
+WIDE_PERSISTENT_D = 50   # persistent kernel's wide instantiation (csrc/persistent.hip kWideD)
+
+
+def _wide_fits(n: int, world: int) -> bool:
+    """Every rank's shard fits the wide persistent kernel: at most 256 rows per CU (one register
+    row per thread of one 256-thread block per CU)."""
+    import torch
+    cus = torch.cuda.get_device_properties(nat.require_device()).multi_processor_count
+    return -(-n // world) <= 256 * cus
+
+
+def exchange_engine(d: int, world: int, n: Optional[int] = None) -> str:
     """Engine of a ``world``-rank run at dimension d: 'persistent' (d = 2, 4: one persistent launch
     per rank, winners exchanged in-kernel), 'steps' (other d: launch-per-step kernels in a HIP graph,
-    records exchanged by a mailbox kernel), 'replicated' (d = 2, 4, ST_SHARDED_EXCHANGE=replicated:
+    records exchanged by a mailbox kernel; also d = 50 -- the wide persistent kernel -- when a rank's
+    shard exceeds 256 rows per CU), 'replicated' (d = 2, 4, ST_SHARDED_EXCHANGE=replicated:
     every GPU thins the whole sample; also the d = 2, 4 fallback) or 'rccl' (RCCL all-gather per
     step; forced by ST_SHARDED_EXCHANGE=rccl, and the fallback otherwise)."""
     choice = os.environ.get('ST_SHARDED_EXCHANGE', 'device')
@@ -327,7 +339,9 @@ def exchange_engine(d: int, world: int) -> str:
         return 'replicated'
     if not 2 <= world <= MAX_PEER_RANKS or choice == 'rccl':
         return 'rccl'
-    return 'persistent' if d in (2, 4) else 'steps'
+    if d in (2, 4) or (d == WIDE_PERSISTENT_D and n is not None and _wide_fits(n, world)):
+        return 'persistent'
+    return 'steps'
 
 
 def device_exchange_eligible(d: int, world: int) -> bool:
@@ -547,7 +561,7 @@ def sharded_runner(integrand: SteinIntegrand, n_points: int, group=None, use_gra
     import torch.distributed as dist
     rank, world = _world(group)
     d = integrand.sample.shape[1]
-    engine = exchange_engine(d, world)
+    engine = exchange_engine(d, world, integrand.n)
     note = ''
     if engine == 'replicated':
         runner = ReplicatedGreedy(integrand, n_points)
@@ -576,7 +590,7 @@ def sharded_runner(integrand: SteinIntegrand, n_points: int, group=None, use_gra
             note = 'device exchange timed out; '
         else:
             note = f'device exchange unavailable ({mb.error}); '
-        if engine == 'persistent':
+        if engine == 'persistent' and d in (2, 4):
             runner = ReplicatedGreedy(integrand, n_points)
             runner.launch()
             idx = runner.indices()

@@ -124,7 +124,8 @@ int st_greedy_finalize(const double *cands_in, int32_t nranks, int32_t d, uint32
  * st_mailbox_handshake verifies the round trip (ok_device[0] = 1) before the first run.
  * seq_base: exchange sequence number of this run's step 0; every rank passes the same value and
  * a following run on the same mailboxes uses seq_base + n_points.
- * Returns ST_ERR_UNSUPPORTED when d is not 2 or 4 (use st_greedy_step + RCCL instead); a run
+ * Returns ST_ERR_UNSUPPORTED when d is not 2 or 4, or d = 50 with more than 256 rows per CU in
+ * this rank's block (use st_greedy_step_exchange or st_greedy_step + RCCL instead); a run
  * whose peers do not answer within the kernel's bounded waits poisons idx_out (UINT32_MAX).
  * ---------------------------------------------------------------------------------------- */
 int64_t st_mailbox_bytes(int32_t nranks);

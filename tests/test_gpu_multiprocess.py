@@ -102,6 +102,19 @@ def test_step_device_exchange_processes_share_one_gpu(tmp_path, world, gf, d):
             np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
 
 
+@pytest.mark.parametrize('world,gf', [(2, True), (3, False)])
+def test_wide_persistent_device_exchange_share_one_gpu(tmp_path, world, gf):
+    """d = 50 shards of at most 256 rows per CU: the wide persistent kernel per rank with the
+    in-kernel mailbox exchange (engine 'persistent' -> mode 'device-exchange'), three runs."""
+    mp.spawn(_worker, args=(world, _free_port(), 'gloo', gf, str(tmp_path), 'device', 3, 50), nprocs=world,
+             join=True)
+    for run in range(3):
+        want = _want(gf if run % 2 == 0 else not gf, 50)
+        for r in range(world):
+            assert (tmp_path / f'mode{r}_{run}.txt').read_text() == 'device-exchange'
+            np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
+
+
 def test_replicated_engine_processes_share_one_gpu(tmp_path):
     """ST_SHARDED_EXCHANGE=replicated (also the d = 2, 4 fallback when the device exchange is
     unavailable): every rank thins the whole sample with the single-GPU kernel, indices agree."""

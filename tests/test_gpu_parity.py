@@ -207,6 +207,36 @@ def test_persistent_two_wave_variants_bit_exact(knobs, d, gf):
     assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
 
 
+@pytest.mark.parametrize('gf', [False, True])
+@pytest.mark.parametrize('n', [60_001, 3_001])
+def test_wide_persistent_d50_bit_exact(n, gf):
+    """d = 50 shards of at most 256 rows per CU run the wide persistent kernel (x rows in
+    registers, g rows in LDS): indices and running sums against the C model, and against the
+    launch-per-step path (st_tune key 3 = 0)."""
+    from stein_thinning import _native
+    d, m = 50, 25
+    x, g = _rw_chain(n, d, seed=50 + n % 7)
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    w = None
+    if gf:
+        lw = -0.02 * np.sum(x * x, axis=1)
+        w = np.exp(lw - lw.min())
+    prob = DeviceProblem(s, gs, w, l, tr)
+    idx, A = prob.greedy(m, return_sums=True)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    np.testing.assert_array_equal(idx, cidx)
+    assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
+    _native.lib().st_tune(3, 0)
+    try:
+        sidx, sA = prob.greedy(m, return_sums=True)
+    finally:
+        _native.lib().st_tune(3, -1)
+    np.testing.assert_array_equal(sidx, idx)
+    assert np.array_equal(sA, A)
+
+
 @pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
 def test_persistent_exact_path_outside_fast_range(d, gf):
     """Rows with components outside [2^-60, 2^60] (tiny / huge scores, tiny coordinates) force the
