@@ -106,6 +106,13 @@ CONFIGS = {
 }
 
 
+def _persistent_nt(n_shard: int, d: int) -> int:
+    """Threads per block the persistent kernel picks by default (persistent.hip,
+    launch_greedy_persistent: 512 above kNt512MinRows = 1280 rows per block, one block per CU)."""
+    rows_per_block = -(-n_shard // 256)
+    return 512 if d in (2, 4) and rows_per_block > 1280 else 256
+
+
 def make_integrand(cfg):
     import warnings
     from stein_thinning import thinning as st
@@ -321,7 +328,8 @@ def main():
             roofline = {
                 'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
                 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': traffic,
-                'kernel': f'greedy_persistent<{d},{str(gf).lower()},RT,256>' + (f' x{world} ranks' if sharded else ''),
+                'kernel': f'greedy_persistent<{d},{str(gf).lower()},RT,{_persistent_nt(n // world, d)}>'
+                          + (f' x{world} ranks' if sharded else ''),
                 'kernel_avg_us': round(avg * 1e6, 1), 'kernel_median_us': round(med * 1e6, 1),
                 'timing': f'HIP events on the launch stream around each of the {args.steps} timed thins'
                           + (' (max over ranks)' if sharded else ''),
@@ -331,8 +339,10 @@ def main():
                 'note': ('compute-bound: the persistent kernel keeps the rows in VGPR/AGPR/LDS across the m steps '
                          '(PMC traffic per launch = "traffic", far below the streaming figure), so the roofline is '
                          'fp64 VALU (MI355X fp64 vector peak 78.6 TF = fp64 matrix peak; no MFMA shape fits '
-                         'the per-pair scalar work); one wave per SIMD issues fp64 at ~7-12 cycles '
-                         '(profiles/r01_fp64_rate.log), ~30% of each step is the in-launch exchange'),
+                         'the per-pair scalar work); 512-thread blocks (two waves per SIMD, LDS and streamed '
+                         'rows dealt in 64-row chunks) once a block holds > 1280 rows: one wave per SIMD issues '
+                         'fp64 at only ~7-12 cycles (profiles/r01_fp64_rate.log); ~1/3 of each step is the '
+                         'in-launch exchange'),
                 'hbm_view': {'algorithmic_bytes_per_launch': alg_bytes, 'bytes_per_pair': bytes_per_pair,
                              'achieved_GBs': round(alg_bytes / avg / 1e9, 1), 'peak_GBs': HBM_PEAK_GBS,
                              'frac': round(alg_bytes / avg / 1e9 / HBM_PEAK_GBS, 4)},

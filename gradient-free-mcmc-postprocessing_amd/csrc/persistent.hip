@@ -52,7 +52,7 @@ struct Scratch {          // small per-block scratch at the start of the dynamic
     int64_t i[kMaxPWaves];
     int abort;
     int rowfast;          // wide d: the winner row lies in the fast range (set by the fetching wave)
-    int pad[2];
+    int ctr[2];           // 512-thread blocks: per-step chunk counters (dynamic LDS / streamed rows)
 };
 
 // Per-thread argmin scan: every thread visits its rows in increasing index order, so a candidate
@@ -75,6 +75,21 @@ __device__ __forceinline__ void scan_take_v(double a, uint32_t ia, double& b, ui
     } else {
         scan_take(a, ia, b, ib);
     }
+}
+
+// Order-free form for rows visited out of index order: ties go to the lower index, NaN beats
+// non-NaN and the lower-indexed NaN wins (np.argmin).  NANFREE: no A of the block is NaN.
+template <bool NANFREE>
+__device__ __forceinline__ void scan_take_idx(double a, uint32_t ia, double& b, uint32_t& ib) {
+    bool take;
+    if constexpr (NANFREE) {
+        take = (a < b) | ((a == b) & (ia < ib));
+    } else {
+        const bool na = __builtin_isnan(a), nb = __builtin_isnan(b);
+        take = (a < b) | ((a == b) & (ia < ib)) | (na & !nb) | (na & nb & (ia < ib));
+    }
+    b = take ? a : b;
+    ib = take ? ia : ib;
 }
 
 // value known to be identical in every lane: move it to SGPRs
@@ -151,6 +166,8 @@ struct PersistArgs {
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
     uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
+    int rec_stride;               // record pitch in granules (2 = packed; wider spreads the polled
+                                  // records over more memory channels)
     int64_t row_begin, row_end;   // this rank's rows (global indices); one device: [0, n)
     int rank, nranks;
     uint64_t seq_base;            // exchange sequence number of step 0 (mailbox banks / tags)
@@ -187,6 +204,10 @@ struct PersistArgs {
 // A consumer accepts a record only when both tags match.  Banks alternate by step parity, so a
 // slot's stale content is exactly two steps old (tag t-1): an 8-bit tag cannot alias it.
 constexpr int kRecGranules = 2;
+// bytes between consecutive blocks' records: 256 spreads the 256 polled records of a step over
+// more memory channels than 16-B packing (-0.3 us per step, profiles/r01_sweep_pitch.log)
+constexpr int kDefaultRecPitch = 256;
+constexpr int64_t kNt512MinRows = 1280;
 
 __device__ __forceinline__ uint64_t step_tag(int64_t t) { return (uint64_t)((t + 1) & 0xFF) << 56; }
 
@@ -206,7 +227,7 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 #pragma unroll
         for (int w = 1; w < NT / 64; ++w) take_if_better(sc->v[w], sc->i[w], v, li);
         sc->vblk = v;   // read by every thread after wait_and_pick's barrier
-        uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * kRecGranules;
+        uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * a.rec_stride;
         const uint64_t tag = step_tag(t);
         const uint64_t vb = (uint64_t)__double_as_longlong(v);
         const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
@@ -235,7 +256,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
     ST_STAMP(a, t + 1, 0);
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const uint64_t* bank = a.gran + (t & 1) * (int64_t)G * kRecGranules;
+        const uint64_t* bank = a.gran + (t & 1) * (int64_t)G * a.rec_stride;
         const uint64_t want = step_tag(t);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t need = 0;
@@ -264,7 +285,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         unsigned it = 0;
         // one 16-B sc1 buffer load per record (both granules; a torn pair fails its tag check)
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bank), 0,
-                                                            G * kRecGranules * 8, 0x00020000);
+                                                            G * a.rec_stride * 8, 0x00020000);
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
         for (;; ++it) {
             // all four loads unconditionally (records past G read as zeros: the descriptor's range
@@ -272,7 +293,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             u32x4 qs[MAXG / 64];
 #pragma unroll
             for (int c = 0; c < MAXG / 64; ++c)
-                qs[c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (lane + 64 * c) * kRecGranules * 8,
+                qs[c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (lane + 64 * c) * a.rec_stride * 8,
                                                               0, 16 /* sc1 */);
 #pragma unroll
             for (int c = 0; c < MAXG / 64; ++c) {
@@ -418,6 +439,11 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     constexpr int kMaxG = 256 * BPC;     // records swept per step
     constexpr bool kTwoWaves = NT >= 512 || BPC > 1;   // two waves per SIMD
     constexpr bool kWide = D > kMaxCtDim;              // register rows only (host guarantees it)
+    // one 512-thread block per CU: the LDS and streamed rows are dealt to the waves in 64-row
+    // chunks from a block counter, so the waves the SIMD arbiter favours take more of them and
+    // all eight finish together (a static split leaves the younger wave of each SIMD running
+    // alone for ~3 us of every step: profiles/r01_stamps_nt512_rt8_rt6_n2e6.log)
+    constexpr bool kDyn = NT >= 512 && BPC == 1 && !kWide;
     extern __shared__ __attribute__((aligned(16))) double lds[];
     Scratch* sc = reinterpret_cast<Scratch*>(lds);
     const int RL = a.RL;
@@ -473,6 +499,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             for (int k = 0; k < D; ++k) rok &= fast_range_ok(a.x[k * ld + row]) & fast_range_ok(a.g[k * ld + row]);
         }
     }
+    if (tid == 0) { sc->ctr[0] = 0; sc->ctr[1] = 0; }
     const int block_fast = __syncthreads_and(rok);
 
     // ---- step 0: diagonal --------------------------------------------------------------------
@@ -526,6 +553,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
         const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, t - 1);
         if (win < 0) break;
         if (blockIdx.x == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
+        // chunk counter of the NEXT step (its last use, step t - 1, ended before publish's barrier)
+        if (kDyn && tid == 0) sc->ctr[(t + 1) & 1] = 0;
         // small d: the winner row in SGPRs (VALU fp64 ops take one scalar operand); wide d: read
         // from LDS inside the pair loop (block-uniform broadcast reads)
         double xj_r[kWide ? 1 : D], gj_r[kWide ? 1 : D];
@@ -579,7 +608,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             };
             // (with two waves per SIMD the registers are too tight to carry the prefetched pair
             // through the on-chip rows: the 512-thread variant issues it after them)
-            constexpr bool kEarlyStream = !kTwoWaves;
+            constexpr bool kEarlyStream = !kTwoWaves && !kDyn;
             int64_t srow = str_base + tid;
             // opaque per step: otherwise LICM hoists the ~20 64-bit load addresses of the first
             // streamed pair out of the step loop and they end up spilled to scratch
@@ -623,52 +652,109 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                 sa[e] = av;
                 return av;
             };
-            // (two waves per SIMD: two chains per wave are enough and leave room for the rows)
-            constexpr int UL = kTwoWaves ? 2 : 4;
-            int e = tid;
-            for (; e + (UL - 1) * kPBlock < RL; e += UL * kPBlock) {
-                double av[UL];
-#pragma unroll
-                for (int u = 0; u < UL; ++u) av[u] = lds_pair(e + u * kPBlock);
-#pragma unroll
-                for (int u = 0; u < UL; ++u)
-                    scan_take_v<FAST>(av[u], (uint32_t)(lds_base + e + u * kPBlock), bv, bi);
-            }
-            for (; e < RL; e += kPBlock) scan_take_v<FAST>(lds_pair(e), (uint32_t)(lds_base + e), bv, bi);
-            ST_STAMP_AFTER(a, t, 6, bv);
             // streamed rows: two per iteration, the next two rows' loads in flight meanwhile
             auto stream_pair = [&](const SRow& r) -> double {
                 double kv = pair_value_ct<D, FAST>(r.x, r.g, xj, gj, l, l2, tr);
                 if constexpr (GF) kv = (kv * r.w) * wj;
                 return add_twice<FAST>(r.a, kv);
             };
-            if constexpr (kTwoWaves) {
-                // two waves per SIMD: one row at a time, no prefetch registers (the other wave
-                // computes while this one waits for its loads)
-                for (; srow < r1; srow += kPBlock) {
-                    SRow r;
-                    fetch(srow, r);
-                    const double av = stream_pair(r);
-                    a.A[srow] = av;
-                    scan_take_v<FAST>(av, (uint32_t)srow, bv, bi);
+            if constexpr (kDyn) {
+                // chunk c < nS: streamed rows [str_base + 64c, +64); c >= nS: LDS rows
+                // [64(c - nS), +64).  Streamed chunks go first: the waves the arbiter favours reach
+                // them while the others still compute register rows, which hides the HBM latency.
+                // A thread's chunk rows are not visited in index order, so their scan compares
+                // indices on ties (scan_take_idx); all of them follow the register rows.
+                const int lane = tid & 63;
+                const int nL = RL >> 6;
+                const int64_t ns = r1 - str_base;
+                const int nS = ns > 0 ? (int)((ns + 63) >> 6) : 0;
+                const int nC = nS + nL;
+                int* ctr = &sc->ctr[t & 1];
+                auto grab = [&]() -> int {
+                    int c = 0;
+                    if (lane == 0)
+                        c = __hip_atomic_fetch_add(ctr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    return __builtin_amdgcn_readfirstlane(c);
+                };
+                auto take_stream = [&](int64_t row, double av) {
+                    if (row < r1) {
+                        a.A[row] = av;
+                        scan_take_idx<FAST>(av, (uint32_t)row, bv, bi);
+                    }
+                };
+                auto one_chunk = [&](int c) {
+                    if (c < nS) {
+                        const int64_t s0 = str_base + ((int64_t)c << 6) + lane;
+                        SRow ra;
+                        fetch(s0, ra);
+                        take_stream(s0, stream_pair(ra));
+                    } else {
+                        const int e0 = ((c - nS) << 6) + lane;
+                        scan_take_idx<FAST>(lds_pair(e0), (uint32_t)(lds_base + e0), bv, bi);
+                    }
+                };
+                for (int c = grab(); c < nC; c = grab()) {
+                    if (c + 1 < nS) {            // two streamed chunks: both loads in flight
+                        const int64_t s0 = str_base + ((int64_t)c << 6) + lane, s1 = s0 + 64;
+                        SRow ra, rb;
+                        fetch(s0, ra);
+                        fetch(s1, rb);
+                        const double av0 = stream_pair(ra), av1 = stream_pair(rb);
+                        take_stream(s0, av0);
+                        take_stream(s1, av1);
+                    } else if (c >= nS && c + 1 < nC) {   // two LDS chunks: two chains
+                        const int e0 = ((c - nS) << 6) + lane, e1 = e0 + 64;
+                        const double av0 = lds_pair(e0), av1 = lds_pair(e1);
+                        scan_take_idx<FAST>(av0, (uint32_t)(lds_base + e0), bv, bi);
+                        scan_take_idx<FAST>(av1, (uint32_t)(lds_base + e1), bv, bi);
+                    } else {                     // the stream/LDS seam or the last chunk
+                        one_chunk(c);
+                        if (c + 1 < nC) one_chunk(c + 1);
+                    }
                 }
-            }
-            while (!kTwoWaves && srow < r1) {
-                const int64_t nrow = srow + 2 * kPBlock;
-                SRow n0, n1;
-                fetch(nrow, n0);
-                fetch(nrow + kPBlock, n1);
-                const double av0 = stream_pair(c0);
-                const double av1 = stream_pair(c1);
-                const bool ok1 = srow + kPBlock < r1;
-                a.A[srow] = av0;
-                if (ok1) a.A[srow + kPBlock] = av1;
-                scan_take_v<FAST>(av0, (uint32_t)srow, bv, bi);
-                scan_take_v<FAST>(ok1 ? av1 : INFINITY, (uint32_t)(srow + kPBlock), bv, bi);
-                c0 = n0;
-                c1 = n1;
-                srow = nrow;
-            }
+                ST_STAMP_AFTER(a, t, 6, bv);
+            } else {
+                // (two waves per SIMD: two chains per wave are enough and leave room for the rows)
+                constexpr int UL = kTwoWaves ? 2 : 4;
+                int e = tid;
+                for (; e + (UL - 1) * kPBlock < RL; e += UL * kPBlock) {
+                    double av[UL];
+#pragma unroll
+                    for (int u = 0; u < UL; ++u) av[u] = lds_pair(e + u * kPBlock);
+#pragma unroll
+                    for (int u = 0; u < UL; ++u)
+                        scan_take_v<FAST>(av[u], (uint32_t)(lds_base + e + u * kPBlock), bv, bi);
+                }
+                for (; e < RL; e += kPBlock) scan_take_v<FAST>(lds_pair(e), (uint32_t)(lds_base + e), bv, bi);
+                ST_STAMP_AFTER(a, t, 6, bv);
+                if constexpr (kTwoWaves) {
+                    // two waves per SIMD: one row at a time, no prefetch registers (the other wave
+                    // computes while this one waits for its loads)
+                    for (; srow < r1; srow += kPBlock) {
+                        SRow r;
+                        fetch(srow, r);
+                        const double av = stream_pair(r);
+                        a.A[srow] = av;
+                        scan_take_v<FAST>(av, (uint32_t)srow, bv, bi);
+                    }
+                }
+                while (!kTwoWaves && srow < r1) {
+                    const int64_t nrow = srow + 2 * kPBlock;
+                    SRow n0, n1;
+                    fetch(nrow, n0);
+                    fetch(nrow + kPBlock, n1);
+                    const double av0 = stream_pair(c0);
+                    const double av1 = stream_pair(c1);
+                    const bool ok1 = srow + kPBlock < r1;
+                    a.A[srow] = av0;
+                    if (ok1) a.A[srow + kPBlock] = av1;
+                    scan_take_v<FAST>(av0, (uint32_t)srow, bv, bi);
+                    scan_take_v<FAST>(ok1 ? av1 : INFINITY, (uint32_t)(srow + kPBlock), bv, bi);
+                    c0 = n0;
+                    c1 = n1;
+                    srow = nrow;
+                }
+            }   // !kDyn
             }   // !kWide
         };
         // the flag is block-uniform (same LDS row, same block flag): make that explicit so the
@@ -706,16 +792,17 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-int64_t persistent_ws_bytes(int d, int G) {
-    // [control: status (and reserved) words][2 banks x G records x 2 granules of 8 B]
+int64_t persistent_ws_bytes(int d, int G, int rec_stride) {
+    // [control: status (and reserved) words][2 banks x G records, rec_stride granules of 8 B apart]
     (void)d;
-    return kWsControlBytes + 2 * (int64_t)G * kRecGranules * 8;
+    return kWsControlBytes + 2 * (int64_t)G * rec_stride * 8;
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
 static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (256)
 static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (one per CU)
 static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
+static int g_persist_pitch = -1; // st_tune key 9: record pitch in bytes (16 .. 4096, power of 2), -1 auto
 static uint64_t* g_stamps = nullptr;
 #ifdef ST_PERSIST_STAMPS
 extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
@@ -739,6 +826,11 @@ int persistent_tune(int key, int value) {
     if (key == 8) {
         if (value != -1 && value != 1 && value != 2) return -1;
         g_persist_bpc = value;
+        return 0;
+    }
+    if (key == 9) {
+        if (value != -1 && (value < 16 || value > 4096 || (value & (value - 1)))) return -1;
+        g_persist_pitch = value;
         return 0;
     }
     return -1;
@@ -809,16 +901,23 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         lds_optin > lds_max)
         lds_max = lds_optin;
     if (lds_max > 163840) lds_max = 163840;
-    const int nt = wide ? 256 : (g_persist_nt > 0 ? g_persist_nt : 256);
+    int nt = wide ? 256 : (g_persist_nt > 0 ? g_persist_nt : 256);
     const int bpc = (!wide && nt == 256 && g_persist_bpc == 2) ? 2 : 1;
     int G = cus * bpc > kMaxGrid ? kMaxGrid : cus * bpc;
     if (g_persist_grid > 0 && G > g_persist_grid) G = g_persist_grid;
     const int64_t min_rows = 256;   // fewer blocks for small n: exchange cost grows with G
     if (n_shard < (int64_t)G * min_rows) G = (int)((n_shard + min_rows - 1) / min_rows);
     if (G < 1) G = 1;
-    if (persistent_ws_bytes(d, G) > ws_bytes) return hipErrorNotSupported;
+    // record pitch: the widest requested / default that the workspace holds (>= 16 B)
+    int pitch = (g_persist_pitch > 0 ? g_persist_pitch : kDefaultRecPitch) / 8;
+    while (pitch > kRecGranules && persistent_ws_bytes(d, G, pitch) > ws_bytes) pitch /= 2;
+    if (persistent_ws_bytes(d, G, pitch) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n_shard + G - 1) / G;
     if (wide && R > 256) return hipErrorNotSupported;   // wide: one register row per thread only
+    // auto: 512-thread blocks (two waves per SIMD, dynamic chunks) once a block has more rows than
+    // one wave per SIMD keeps in registers comfortably (measured crossover 1e3 .. 2e3 rows per CU,
+    // scripts/sweep_nt_crossover.sh)
+    if (!wide && g_persist_nt <= 0 && bpc == 1 && R > kNt512MinRows) nt = 512;
     const int rt_max = (nt == 512 || bpc == 2) ? 8 : 16;
     int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
     if (rt != 4 && rt != 6 && rt != 8 && rt != 16) rt = rt_max;
@@ -849,6 +948,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.gran = reinterpret_cast<uint64_t*>(p + kWsControlBytes);
     a.rows_per_block = R;
     a.RL = (int)RL;
+    a.rec_stride = pitch;
     a.stamps = g_stamps;
     a.row_begin = rs->row_begin;
     a.row_end = rs->row_end;
@@ -858,7 +958,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.inbox = rs->inbox;
     for (int r = 0; r < kMaxRanks; ++r) a.peer[r] = r < rs->nranks ? rs->peer[r] : nullptr;
     // zero status and every granule tag (a stale tag from a previous run must never match)
-    hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G), s);
+    hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G, pitch), s);
     if (e != hipSuccess) return e;
     if (wide) e = gf ? launch_p<kWideD, true, 1, 256>(a, G, lds, s) : launch_p<kWideD, false, 1, 256>(a, G, lds, s);
     else if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s);

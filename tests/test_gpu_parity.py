@@ -179,6 +179,9 @@ def test_persistent_and_fallback_bit_exact(tune):
     ('two blocks per CU, 4 register rows', {8: 2, 3: 4}),
     ('512-thread blocks, 8 register rows', {4: 512, 3: 8}),
     ('512-thread blocks, 6 register rows', {4: 512, 3: 6}),
+    ('512-thread blocks, 4 register rows', {4: 512, 3: 4}),
+    ('256-thread blocks (one wave per SIMD), LDS and streamed rows', {4: 256}),
+    ('512-thread blocks, packed 16-B records', {4: 512, 9: 16}),
 ])
 @pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
 def test_persistent_two_wave_variants_bit_exact(knobs, d, gf):
@@ -200,7 +203,7 @@ def test_persistent_two_wave_variants_bit_exact(knobs, d, gf):
     try:
         idx, A = DeviceProblem(s, gs, w, l, tr).greedy(m, return_sums=True)
     finally:
-        for k in (3, 4, 8):
+        for k in (3, 4, 8, 9):
             L.st_tune(k, -1)
     cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
     np.testing.assert_array_equal(idx, cidx)

@@ -1,7 +1,7 @@
 """Persistent-kernel variant sweep on one GPU: time st_greedy for the bench configs under several
 st_tune settings and check that every variant selects the same indices.
 
-    python tools/tune_sweep.py [c4|c2|c3] "8=1" "8=2" "8=2,3=4" ...
+    python tools/tune_sweep.py [c4|c2|c3|c4@<n>] "8=1" "8=2" "8=2,3=4" ...
 Each argument is a comma-separated list of key=value st_tune settings (reset to -1 between)."""
 import os
 import sys
@@ -18,14 +18,18 @@ from stein_thinning import _native as nat  # noqa: E402
 
 cfg_name = sys.argv[1] if len(sys.argv) > 1 and not '=' in sys.argv[1] else 'c4'
 settings = [a for a in sys.argv[1:] if '=' in a] or ['8=1', '8=2']
-cfg = bench.CONFIGS[cfg_name]
+# "c4@1000000": config 4's data and m at another n (crossover sweeps)
+base, _, n_over = cfg_name.partition('@')
+cfg = dict(bench.CONFIGS[base])
+if n_over:
+    cfg['n'] = int(float(n_over))
 integrand, _, _ = bench.make_integrand(cfg)
 prob = integrand.device_problem()
 m = cfg['m']
 L = nat.lib()
 ref = None
 for st in settings:
-    for k in (3, 4, 5, 8):
+    for k in (3, 4, 5, 8, 9):
         L.st_tune(k, -1)
     for kv in st.split(','):
         k, v = (int(x) for x in kv.split('='))
