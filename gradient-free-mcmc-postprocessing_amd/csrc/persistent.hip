@@ -289,12 +289,17 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
         for (;; ++it) {
             // all four loads unconditionally (records past G read as zeros: the descriptor's range
-            // check), so they issue back to back and a poll costs ONE round trip, not four
+            // check), so they issue back to back and a poll costs ONE round trip, not four; a record
+            // already seen is re-read at an out-of-range offset (zeros, no memory access), so later
+            // polls only load what is still missing
             u32x4 qs[MAXG / 64];
+            const uint32_t oob = (uint32_t)G * a.rec_stride * 8;
 #pragma unroll
-            for (int c = 0; c < MAXG / 64; ++c)
-                qs[c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (lane + 64 * c) * a.rec_stride * 8,
+            for (int c = 0; c < MAXG / 64; ++c) {
+                const uint32_t off = (uint32_t)(lane + 64 * c) * a.rec_stride * 8;
+                qs[c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((need & ~seen) >> c) & 1u ? off : oob,
                                                               0, 16 /* sc1 */);
+            }
 #pragma unroll
             for (int c = 0; c < MAXG / 64; ++c) {
                 if ((need & ~seen) & (1u << c)) {
