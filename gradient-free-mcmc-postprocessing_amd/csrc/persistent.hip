@@ -681,11 +681,19 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                         c = __hip_atomic_fetch_add(ctr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     return __builtin_amdgcn_readfirstlane(c);
                 };
+                // branch-free tail handling, so the two streamed chunks of an iteration stay in one
+                // basic block with all their loads issued up front: rows past r1 store through a
+                // buffer descriptor that ends at r1 (dropped by the range check) and scan as +inf
+                // with the largest index
+                const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(
+                    a.A + str_base, 0, ns > 0 ? (int)(ns * 8) : 0, 0x00020000);
                 auto take_stream = [&](int64_t row, double av) {
-                    if (row < r1) {
-                        a.A[row] = av;
-                        scan_take_idx<FAST>(av, (uint32_t)row, bv, bi);
-                    }
+                    const bool in = row < r1;
+                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                    const uint64_t ab = (uint64_t)__double_as_longlong(av);
+                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{(unsigned)ab, (unsigned)(ab >> 32)}, arsrc,
+                                                          in ? (int)((row - str_base) * 8) : (int)(ns * 8), 0, 0);
+                    scan_take_idx<FAST>(in ? av : INFINITY, in ? (uint32_t)row : 0xFFFFFFFFu, bv, bi);
                 };
                 auto one_chunk = [&](int c) {
                     if (c < nS) {
