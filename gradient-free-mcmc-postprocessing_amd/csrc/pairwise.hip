@@ -95,6 +95,7 @@ __global__ __launch_bounds__(256) void kmat_kernel(PairArgs p, int64_t k, double
 // column: a sequential sum in increasing a.
 // ------------------------------------------------------------------------------------------
 constexpr int kColBlock = 256;
+constexpr int kColsumUnroll = 2;   // rows per iteration of the column-sum sweep
 
 struct ColsumArgs {
     const double* x;
@@ -150,12 +151,26 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
         auto sweep = [&](auto fast_tag) {
             constexpr bool FAST = decltype(fast_tag)::value;
             asm volatile(";; colsum variant" ::);
-            for (int e = 0; e < cnt; ++e) {
+            auto pair_at = [&](int e) -> double {
                 double xa[D], ga[D];
 #pragma unroll
                 for (int k = 0; k < D; ++k) { xa[k] = sx[k][e]; ga[k] = sg[k][e]; }
                 double kv = pair_value_ct<D, FAST>(xi, gi, xa, ga, l, l2, tr);
                 if constexpr (GF) kv = (kv * wi) * sw[e];
+                return kv;
+            };
+            // kColsumUnroll rows per iteration: independent pair chains for the fp64 pipe, summed
+            // into acc in row order (same bits as one row at a time)
+            int e = 0;
+            for (; e + kColsumUnroll <= cnt; e += kColsumUnroll) {
+                double kv[kColsumUnroll];
+#pragma unroll
+                for (int u = 0; u < kColsumUnroll; ++u) kv[u] = pair_at(e + u);
+#pragma unroll
+                for (int u = 0; u < kColsumUnroll; ++u) acc = (ac + e + u < i) ? acc + kv[u] : acc;
+            }
+            for (; e < cnt; ++e) {
+                const double kv = pair_at(e);
                 acc = (ac + e < i) ? acc + kv : acc;
             }
         };
