@@ -162,3 +162,44 @@ def test_tiny_shards_and_more_points_than_rows(tmp_path, world, exchange, d):
     for r in range(world):
         np.testing.assert_array_equal(np.load(tmp_path / f'small{r}.npy'), want)
         assert (tmp_path / f'smallmode{r}.txt').read_text() == expect
+
+
+def _large_worker(rank, world, port, out_dir, n, m):
+    """One rank of a device-exchange run whose shards exceed 1 280 rows per block (the 512-thread,
+    dynamic-chunk persistent kernel with LDS and streamed rows); grids capped so that the ranks'
+    one-block-per-CU grids co-reside on the shared GPU (as bench.py's rehearsal mode does)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from stein_thinning import _native as nat
+        from stein_thinning import distributed as sd
+        assert nat.lib().st_tune(5, 256 // world) == 0
+        x, g = _rw_data(n)
+        idx = sd.thin_sharded(x, g, m, preconditioner='med')
+        np.save(os.path.join(out_dir, f'idx{rank}.npy'), idx)
+        with open(os.path.join(out_dir, f'mode{rank}.txt'), 'w') as f:
+            f.write(str(sd.last_mode))
+    finally:
+        dist.destroy_process_group()
+
+
+def _rw_data(n, d=4):
+    rng = np.random.default_rng(23)
+    x = np.cumsum(0.05 * rng.normal(size=(n, d)), axis=0)   # random-walk chain: near-duplicate rows
+    x[n // 2:n // 2 + 500] = x[1_000:1_500]                  # exact ties across the shard boundary
+    g = -x + 0.1 * rng.normal(size=(n, d))
+    g[n // 2:n // 2 + 500] = g[1_000:1_500]
+    return x, g
+
+
+def test_device_exchange_512_thread_shards_share_one_gpu(tmp_path):
+    """Two ranks, 2e5 rows each on 128 blocks (1 563 rows per block > 1 280): the 512-thread
+    persistent kernel under the device exchange, against the NumPy oracle."""
+    n, m, world = 400_003, 30, 2
+    mp.spawn(_large_worker, args=(world, _free_port(), str(tmp_path), n, m), nprocs=world, join=True)
+    x, g = _rw_data(n)
+    want = o.thin(x, g, m, preconditioner='med')
+    for r in range(world):
+        assert (tmp_path / f'mode{r}.txt').read_text() == 'device-exchange'
+        np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}.npy'), want)
