@@ -21,7 +21,7 @@ run() {
 if [[ ${2:-full} == full ]]; then
   run bench_$CFG 900 python bench.py --config $CFG --steps 5 --warmup 2
 fi
-run trace_$CFG 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$CFG -o trace -- python3 bench.py --config $CFG --steps 2 --warmup 1 --no-cpu-baseline
+run trace_$CFG 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$CFG -o trace -- python3 bench.py --config $CFG --steps 10 --warmup 2 --no-cpu-baseline
 run pmc_fetch_$CFG 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d gpurun_out/pmc_fetch_$CFG -o pmc -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-timing
 run pmc_write_$CFG 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/pmc_write_$CFG -o pmc -- python3 bench.py --config $CFG --steps 1 --warmup 0 --no-cpu-baseline --no-kernel-timing
 echo "=== done"
