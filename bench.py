@@ -552,10 +552,15 @@ def main_proxy(args):
         dist.barrier()
         elapsed, kern_s = _max_over_ranks([elapsed, kern_s], dev)
     if rank == 0:
-        flop_row = 4 * d * d + 2 * d + (2 * d + 12 if t_kind else 2)
+        # algorithmic work of the kernel that runs: 16 < d <= 64 -> the matrix-core kernel (one
+        # product y = P dev per row, Mahalanobis term dev . y: 2d^2 + 2d flop + the epilogue);
+        # otherwise the VALU kernel (z = dev U and y: 4d^2 + 2d)
+        mfma = 16 < d <= 64
+        flop_row = (2 * d * d + 2 * d if mfma else 4 * d * d + 2 * d) + (2 * d + 12 if t_kind else 2)
         bytes_row = 16 * d + 8
         tflops = rows * flop_row / kern_s / 1e12
         gbs = rows * bytes_row / kern_s / 1e9
+        hbm_bound = bytes_row / (HBM_PEAK_GBS * 1e9) >= flop_row / (FP64_VALU_PEAK_TFS * 1e12)
         line = {
             'metric': 'proxy rows/s (log q + grad log q per sample row)', 'value': n * args.steps / elapsed,
             'unit': 'rows/s', 'n_gpus': world, 'steps': args.steps, 'warmup': args.warmup,
@@ -564,12 +569,17 @@ def main_proxy(args):
             'config': {'workload': f"config 5 proxy: {'Student-t df=4' if t_kind else 'Gaussian'} "
                                    'N(mean, 1.2 cov), n=5e5 d=50', 'n': n, 'd': d,
                        'parallelism': f'row blocks x{world}' if world > 1 else 'single-gpu'},
-            'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
-                         'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': None,
-                         'kernel': 'proxy_kernel', 'kernel_avg_us': round(kern_s * 1e6, 1),
-                         'flop_per_row': flop_row, 'bytes_per_row': bytes_row,
-                         'hbm_view': {'achieved_GBs': round(gbs, 1), 'peak_GBs': HBM_PEAK_GBS,
-                                      'frac': round(gbs / HBM_PEAK_GBS, 4)}},
+            'roofline': dict(
+                ({'bound': 'hbm', 'achieved': round(gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+                  'frac': round(gbs / HBM_PEAK_GBS, 4)} if hbm_bound else
+                 {'bound': 'mfma' if mfma else 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
+                  'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4)}),
+                traffic=None, kernel='proxy_mfma_kernel' if mfma else 'proxy_kernel',
+                kernel_avg_us=round(kern_s * 1e6, 1), flop_per_row=flop_row, bytes_per_row=bytes_row,
+                fp64_view={'achieved_TFs': round(tflops, 2), 'peak_TFs': FP64_VALU_PEAK_TFS,
+                           'frac': round(tflops / FP64_VALU_PEAK_TFS, 4)},
+                hbm_view={'achieved_GBs': round(gbs, 1), 'peak_GBs': HBM_PEAK_GBS,
+                          'frac': round(gbs / HBM_PEAK_GBS, 4)}),
         }
         if world == 1 and not args.no_cpu_baseline:
             from oracle import proxy_numpy as op

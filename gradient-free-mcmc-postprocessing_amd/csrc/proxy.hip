@@ -136,33 +136,28 @@ __global__ __launch_bounds__(kThreads) void proxy_kernel(ProxyArgs a) {
     }
 }
 
-// ---- 16 < d <= 64: the two (64, d) x (d, d) products of a row tile on the matrix cores ---------
+// ---- 16 < d <= 64: the (64, d) x (d, d) product of a row tile on the matrix cores ----------------
 // v_mfma_f64_16x16x4_f64 (gfx950 maps, cdna_hip_programming.md: A[l&15][k=l>>4], B[k=l>>4][l&15],
-// D col = l&15, row = (l>>4) + 4 reg).  Output columns: T = 2 ceil(d/16) tiles of 16 (z = dev @ U
-// tiles, then y = dev @ P^T tiles), wave w owns tiles w and w + 4; its B fragments (all k-steps)
-// stay in VGPRs for the life of the block, which loops over 64-row tiles (persistent grid).  Per
-// tile: the x tile is staged (coalesced) into LDS as dev = x - loc, each wave runs S = ceil(d/4)
-// k-steps x 4 row subtiles x its tiles of MFMAs, z^2 is reduced across the 16 column lanes, y goes
-// back through LDS and out as contiguous grad rows.
+// D col = l&15, row = (l>>4) + 4 reg).  One product per tile: y = dev @ P^T in T = ceil(d/16) column
+// tiles of 16, wave w owning tile w (its B fragments, all k-steps, in VGPRs for the life of the
+// block, which loops over 64-row tiles: persistent grid).  The Mahalanobis term is dev . y (the
+// same quadratic form as scipy's |dev @ U|^2, U U^T = pinv(cov) = P for the full-rank covariances
+// the proxies use; fp64 tolerance like the other summation-order differences), reduced across the
+// 16 column lanes with DPP and across the waves through LDS -- one matrix product per row instead
+// of two.  Per tile: the x tile is staged (coalesced) into LDS as dev = x - loc, each wave runs
+// S = ceil(d/4) k-steps x 4 row subtiles of MFMAs, y goes back through LDS and out as contiguous
+// grad rows.
 constexpr int kMfmaMaxD = 64;
 constexpr int kMfmaMaxS = kMfmaMaxD / 4;
 typedef double dbl4 __attribute__((ext_vector_type(4)));
 
-// sum over the 16 lanes of a DPP row (every lane gets the total): quad xor 1, quad xor 2, half-row
-// mirror, row mirror -- VALU data movement instead of LDS permutes
+// one DPP lane permutation of a double (quad_perm controls: VALU data movement, no LDS permute)
 template <int CTRL>
 __device__ inline double dpp_f64(double v) {
     const long long b = __double_as_longlong(v);
     const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xF, 0xF, false);
     const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xF, 0xF, false);
     return __longlong_as_double(((long long)hi << 32) | (unsigned)lo);
-}
-__device__ inline double row16_sum(double v) {
-    v += dpp_f64<0xB1>(v);    // quad_perm [1,0,3,2]
-    v += dpp_f64<0x4E>(v);    // quad_perm [2,3,0,1]
-    v += dpp_f64<0x141>(v);   // row_half_mirror
-    v += dpp_f64<0x140>(v);   // row_mirror
-    return v;
 }
 
 __host__ __device__ inline int mfma_pitch(int dk) { return ((dk + 27) / 32) * 32 + 4; }   // = 4 mod 32 doubles
@@ -174,7 +169,7 @@ __global__ __launch_bounds__(kThreads, 2) void proxy_mfma_kernel(ProxyArgs a) {
     const int dk = 4 * S;
     const int PD = mfma_pitch(dk);
     const int PY = d + 1;
-    const int tz = (d + 15) / 16;            // z tiles (= y tiles)
+    const int tz = (d + 15) / 16;            // y column tiles of 16
     double* s_dev = lds;                      // [64][PD]
     double* s_y = s_dev + kRows * PD;         // [64][PY]
     double* s_part = s_y + kRows * PY;        // [4][64]
@@ -189,23 +184,13 @@ __global__ __launch_bounds__(kThreads, 2) void proxy_mfma_kernel(ProxyArgs a) {
     const int lane = tid & 63;
     const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int li = lane & 15, lk = lane >> 4;
-    // owned tiles: t0 = w, t1 = w + 4 (tile t < tz: z tile t; else y tile t - tz)
-    const int T = 2 * tz;
-    const bool has0 = w < T, has1 = w + 4 < T;
-    double b0[kMfmaMaxS], b1[kMfmaMaxS];
-    auto bval = [&](int t, int s) -> double {
-        const int k = 4 * s + lk;
-        if (t < tz) {
-            const int j = 16 * t + li;
-            return (k < d && j < d) ? a.U[(int64_t)k * d + j] : 0.0;
-        }
-        const int j = 16 * (t - tz) + li;
-        return (k < d && j < d) ? a.P[(int64_t)j * d + k] : 0.0;
-    };
+    const bool has = w < tz;                  // wave w owns y tile w (tz <= 4 for d <= 64)
+    const int jcol = 16 * w + li;             // this lane's output column
+    double bf[kMfmaMaxS];
 #pragma unroll
     for (int s = 0; s < kMfmaMaxS; ++s) {
-        b0[s] = (has0 && s < S) ? bval(w, s) : 0.0;
-        b1[s] = (has1 && s < S) ? bval(w + 4, s) : 0.0;
+        const int k = 4 * s + lk;
+        bf[s] = (has && s < S && k < d && jcol < d) ? a.P[(int64_t)jcol * d + k] : 0.0;
     }
     const float inv_d = 1.0f / (float)d;
     const int64_t ntiles = (a.n + kRows - 1) / kRows;
@@ -237,77 +222,50 @@ __global__ __launch_bounds__(kThreads, 2) void proxy_mfma_kernel(ProxyArgs a) {
         }
         __syncthreads();
         if (tile + gridDim.x < ntiles) prefetch(tile + gridDim.x);   // overlaps this tile's MFMAs
-        // two passes of 32 rows (2 row subtiles each) keep the accumulators at 16 doubles
-#pragma unroll 1
-        for (int half = 0; half < 2; ++half) {
-            dbl4 acc0[2], acc1[2];
+        // all four 16-row subtiles in one pass: four independent accumulator chains
+        dbl4 acc[4];
 #pragma unroll
-            for (int u = 0; u < 2; ++u) { acc0[u] = dbl4{0, 0, 0, 0}; acc1[u] = dbl4{0, 0, 0, 0}; }
+        for (int u = 0; u < 4; ++u) acc[u] = dbl4{0, 0, 0, 0};
+        if (has) {
 #pragma unroll
             for (int s = 0; s < kMfmaMaxS; ++s) {
                 if (s < S) {
-                    double av[2];
+                    double av[4];
 #pragma unroll
-                    for (int u = 0; u < 2; ++u) av[u] = s_dev[(16 * (2 * half + u) + li) * PD + 4 * s + lk];
-                    if (has0) {
+                    for (int u = 0; u < 4; ++u) av[u] = s_dev[(16 * u + li) * PD + 4 * s + lk];
 #pragma unroll
-                        for (int u = 0; u < 2; ++u) acc0[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], b0[s], acc0[u], 0, 0, 0);
-                    }
-                    if (has1) {
-#pragma unroll
-                        for (int u = 0; u < 2; ++u) acc1[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], b1[s], acc1[u], 0, 0, 0);
-                    }
+                    for (int u = 0; u < 4; ++u) acc[u] = __builtin_amdgcn_mfma_f64_16x16x4f64(av[u], bf[s], acc[u], 0, 0, 0);
                 }
             }
-            // epilogue: z tiles -> per-row partial |z|^2 of this wave; y tiles -> s_y
-            double part[2][4];
+        }
+        // epilogue: y -> s_y; then every thread takes a quarter of one row's dot dev . y (columns
+        // j = q, q + 4, ...; row = tid / 4), the four partials summed with two quad DPP steps
+        if (has && jcol < d) {
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int u = 0; u < 4; ++u)
 #pragma unroll
-                for (int r = 0; r < 4; ++r) part[u][r] = 0.0;
-            auto take = [&](int t, dbl4* acc) {
-                if (t < tz) {
-#pragma unroll
-                    for (int u = 0; u < 2; ++u)
-#pragma unroll
-                        for (int r = 0; r < 4; ++r) part[u][r] = fma(acc[u][r], acc[u][r], part[u][r]);
-                } else {
-                    const int j = 16 * (t - tz) + li;
-                    if (j < d) {
-#pragma unroll
-                        for (int u = 0; u < 2; ++u)
-#pragma unroll
-                            for (int r = 0; r < 4; ++r) s_y[(16 * (2 * half + u) + lk + 4 * r) * PY + j] = acc[u][r];
-                    }
-                }
-            };
-            if (has0) take(w, acc0);
-            if (has1) take(w + 4, acc1);
-#pragma unroll
-            for (int u = 0; u < 2; ++u)
-#pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const double v = row16_sum(part[u][r]);
-                    if (li == 0) s_part[w * kRows + 16 * (2 * half + u) + lk + 4 * r] = v;
-                }
+                for (int r = 0; r < 4; ++r) s_y[(16 * u + lk + 4 * r) * PY + jcol] = acc[u][r];
         }
         __syncthreads();
-        if (w == 0) {
-            const double maha = ((s_part[lane] + s_part[kRows + lane]) + s_part[2 * kRows + lane]) +
-                                s_part[3 * kRows + lane];
-            double lq, coef;
-            if (a.df > 0.0) {
-                double my = 0.0;
-                for (int k = 0; k < d; ++k) my = fma(s_dev[lane * PD + k], s_y[lane * PY + k], my);
-                const double t = 0.5 * (a.df + (double)d);
-                lq = a.c_log + -t * log(1.0 + (1.0 / a.df) * maha);
-                coef = (-(a.df + (double)d) / a.df) / (1.0 + my / a.df);
-            } else {
-                lq = -0.5 * (a.c_log + maha);
-                coef = -1.0;
+        {
+            const int row = tid >> 2, q = tid & 3;
+            double part = 0.0;
+            for (int j = q; j < d; j += 4) part = fma(s_dev[row * PD + j], s_y[row * PY + j], part);
+            part += dpp_f64<0xB1>(part);    // quad_perm [1,0,3,2]
+            const double maha = part + dpp_f64<0x4E>(part);   // quad_perm [2,3,0,1]
+            if (q == 0) {
+                double lq, coef;
+                if (a.df > 0.0) {
+                    const double t = 0.5 * (a.df + (double)d);
+                    lq = a.c_log + -t * log(1.0 + (1.0 / a.df) * maha);
+                    coef = (-(a.df + (double)d) / a.df) / (1.0 + maha / a.df);
+                } else {
+                    lq = -0.5 * (a.c_log + maha);
+                    coef = -1.0;
+                }
+                if (row < rows) a.log_q[r0 + row] = lq;
+                s_coef[row] = coef;
             }
-            if (lane < rows) a.log_q[r0 + lane] = lq;
-            s_coef[lane] = coef;
         }
         __syncthreads();
         double* gb = a.grad + r0 * d;
