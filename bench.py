@@ -20,9 +20,12 @@ rows), ten pooled chains of 2e5 for n=2e6.
 from __future__ import annotations
 
 import argparse
+import faulthandler
 import json
 import os
 import platform
+import socket
+import subprocess
 import sys
 import time
 
@@ -34,7 +37,8 @@ for _p in (ROOT, PKG_ROOT):
     if _p not in sys.path:
         sys.path.insert(0, _p)
 
-BASELINE = json.load(open(os.path.join(ROOT, 'BASELINE.json')))
+with open(os.path.join(ROOT, 'BASELINE.json')) as _f:
+    BASELINE = json.load(_f)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 FP64_VALU_PEAK_TFS = 78.6  # MI355X spec fp64 vector (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz)
 
@@ -216,7 +220,35 @@ def _max_over_ranks(values, dev):
     return [float(v) for v in t.tolist()]
 
 
+def algorithmic_flop_per_pair(d: int, gf: bool) -> int:
+    """Algorithmic fp64 work of one Stein-kernel pair, SURVEY.md section 8(d): 12 d + 40 flop
+    (isotropic Gamma^-1; the per-coordinate products and sums of vfk0_imq,
+    JAX_Stein_Thinning.ipynb:354-361, plus the constant tail of 2 pow, 1 sqrt, 3 divisions); the
+    gradient-free weights w_i w_j add 2 multiplies.  88 at d = 4, 640 at d = 50.  This is the
+    figure `roofline.frac` is priced on; the kernels' ISA count (correctly rounded powers in
+    double-double, Newton steps of the divisions) is reported beside it as `issue`."""
+    return 12 * d + 40 + (2 if gf else 0)
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(('127.0.0.1', 0))
+        return s.getsockname()[1]
+
+
+def _launch_ranks(argv) -> int:
+    """`--gpus N` without a launcher: run N ranks under torch.distributed.run as a child process
+    (this process never touches the GPU) and return its exit code; rank 0 prints the JSON line."""
+    import re
+    m = re.search(r'--gpus[ =](\d+)', ' '.join(argv))
+    n = int(m.group(1)) if m else 1
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={n}',
+           '--master-addr', '127.0.0.1', '--master-port', str(_free_port()), os.path.abspath(__file__)] + argv
+    return subprocess.call(cmd)
+
+
 def main():
+    faulthandler.enable()   # a crash (e.g. under rocprofv3) leaves the Python stack in the log
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=5, help='timed thins')
@@ -229,10 +261,21 @@ def main():
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
-    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv'],
+    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'ranks'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
-                         '(row-sharded, RCCL all-reduce of the n-length column-sum vector)')
+                         '(row-sharded, RCCL all-reduce of the n-length column-sum vector); ranks: launcher '
+                         'check only (gloo, no GPU)')
     args = ap.parse_args()
+    if args.gpus < 1:
+        ap.error('--gpus must be >= 1')
+    env_world = os.environ.get('WORLD_SIZE')
+    if env_world is None and args.gpus > 1:
+        return _launch_ranks(sys.argv[1:])
+    if env_world is not None and int(env_world) != args.gpus:
+        print(f'bench.py: WORLD_SIZE={env_world} but --gpus {args.gpus}', file=sys.stderr)
+        return 2
+    if args.workload == 'ranks':
+        return main_ranks(args)
     if args.workload == 'ksd':
         return main_ksd(args)
     if args.workload == 'proxy':
@@ -301,13 +344,14 @@ def main():
     if rank == 0 or sharded:
         gf = integrand.weights is not None
         bytes_per_pair = 16 * d + (24 if gf else 16)
-        # fp64 work per pair of the persistent kernel's hot loop, counted in its ISA
-        # (greedy_persistent<4,false,16,256>, range-guarded variant): 38 v_mul_f64 + 26 v_add_f64
-        # + 33 v_fma/v_fmac_f64 + 3 v_rcp_f64 + 1 v_rsq_f64 = 101 fp64 VALU instructions,
-        # 134 flop (fma = 2); each further coordinate adds 13 (2 sub, 6 mul, 3 add, 1 mul + 1 add
-        # of the score product); the gradient-free weights add 2 mul
+        # algorithmic work per pair: what `frac` is priced on
+        flop_per_pair = algorithmic_flop_per_pair(d, gf)
+        # what the persistent kernel's hot loop actually issues, counted in its ISA
+        # (greedy_persistent<4,false,8,512>): 38 v_mul_f64 + 26 v_add_f64 + 33 v_fma/v_fmac_f64
+        # + 3 v_rcp_f64 + 1 v_rsq_f64 = 101 fp64 VALU instructions, 134 flop (fma = 2); each further
+        # coordinate adds 13; the gradient-free weights add 2 mul
         instr_per_pair = 101 + 13 * (d - 4) + (2 if gf else 0)
-        flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0)
+        issue_flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0)
         pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
         pmc_rec = json.load(open(pmc)) if os.path.exists(pmc) else {}
         if persistent:
@@ -319,8 +363,8 @@ def main():
             if sharded:
                 avg, med = _max_over_ranks([avg, med], dev)
             pairs_launch = n * m / world          # per rank
-            tflops = pairs_launch * flop_per_pair / avg / 1e12
-            gins = pairs_launch * instr_per_pair / avg / 1e12
+            tflops = pairs_launch * flop_per_pair / med / 1e12
+            gins = pairs_launch * instr_per_pair / med / 1e12
             issue_peak = 256 * 4 * 16 * 2.4e9 / 1e12   # fp64 lane-instructions/s (T), 4 cycles per wave-instr
             alg_bytes = int(pairs_launch * bytes_per_pair)
             rec = pmc_rec.get(f'{args.config}_persistent') if world == 1 else None
@@ -330,22 +374,22 @@ def main():
                 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': traffic,
                 'kernel': f'greedy_persistent<{d},{str(gf).lower()},RT,{_persistent_nt(n // world, d)}>'
                           + (f' x{world} ranks' if sharded else ''),
-                'kernel_avg_us': round(avg * 1e6, 1), 'kernel_median_us': round(med * 1e6, 1),
-                'timing': f'HIP events on the launch stream around each of the {args.steps} timed thins'
-                          + (' (max over ranks)' if sharded else ''),
-                'flop_per_pair': flop_per_pair, 'fp64_instr_per_pair': instr_per_pair,
-                'fp64_issue': {'achieved_Tinstr_s': round(gins, 2), 'peak_Tinstr_s': round(issue_peak, 2),
-                               'frac': round(gins / issue_peak, 4)},
+                'kernel_median_us': round(med * 1e6, 1), 'kernel_avg_us': round(avg * 1e6, 1),
+                'timing': f'median of HIP events on the launch stream around each of the {args.steps} timed '
+                          'thins (one persistent launch each)' + (', max over ranks' if sharded else ''),
+                'flop_per_pair': flop_per_pair,
+                'flop_per_pair_source': 'SURVEY.md 8(d): 12 d + 40 (+2 gradient-free), algorithmic',
+                'issue': {'fp64_instr_per_pair': instr_per_pair, 'isa_flop_per_pair': issue_flop_per_pair,
+                          'achieved_TFs': round(pairs_launch * issue_flop_per_pair / med / 1e12, 2),
+                          'achieved_Tinstr_s': round(gins, 2), 'peak_Tinstr_s': round(issue_peak, 2),
+                          'frac': round(gins / issue_peak, 4)},
                 'note': ('compute-bound: the persistent kernel keeps the rows in VGPR/AGPR/LDS across the m steps '
                          '(PMC traffic per launch = "traffic", far below the streaming figure), so the roofline is '
                          'fp64 VALU (MI355X fp64 vector peak 78.6 TF = fp64 matrix peak; no MFMA shape fits '
-                         'the per-pair scalar work); 512-thread blocks (two waves per SIMD, LDS and streamed '
-                         'rows dealt in 64-row chunks) once a block holds > 1280 rows: one wave per SIMD issues '
-                         'fp64 at only ~7-12 cycles (profiles/r01_fp64_rate.log); ~1/3 of each step is the '
-                         'in-launch exchange'),
+                         'the per-pair scalar work); part of each step is the in-launch winner exchange'),
                 'hbm_view': {'algorithmic_bytes_per_launch': alg_bytes, 'bytes_per_pair': bytes_per_pair,
-                             'achieved_GBs': round(alg_bytes / avg / 1e9, 1), 'peak_GBs': HBM_PEAK_GBS,
-                             'frac': round(alg_bytes / avg / 1e9 / HBM_PEAK_GBS, 4)},
+                             'achieved_GBs': round(alg_bytes / med / 1e9, 1), 'peak_GBs': HBM_PEAK_GBS,
+                             'frac': round(alg_bytes / med / 1e9 / HBM_PEAK_GBS, 4)},
             }
         if not sharded and not args.no_kernel_timing:
             s_avg, s_med = kernel_timing(prob, min(m, 200))
@@ -381,6 +425,18 @@ def main():
                    'pair_evals_per_s': n * m / (time.perf_counter() - t_e),
                    'same_indices': bool(np.array_equal(e2e_idx, result_idx))}
 
+    exchange, degraded = None, False
+    if sharded:
+        # the engine the run was meant to use vs the one it ended on (a fallback after a failed
+        # mailbox setup or an expired bounded wait is reported, never silent)
+        engine = runner.engine
+        want = {'persistent': 'device-exchange', 'steps': 'device-exchange-steps-graph',
+                'replicated': 'replicated',
+                'rccl': 'rccl-graph' if dist.get_backend() == 'nccl' else 'records-all-gather'}[engine]
+        exchange = {'engine': engine, 'mode': runner.mode}
+        degraded = runner.mode != want
+        if degraded and rank == 0:
+            print(f'bench.py: DEGRADED exchange: wanted {want}, ran {runner.mode}', file=sys.stderr)
     if rank == 0:
         pairs = float(n) * m * args.steps
         line = {
@@ -402,12 +458,33 @@ def main():
                                        if sharded else 'single-gpu'),
                        'wallclock_thin_s': elapsed / args.steps,
                        'first_indices': result_idx[:8].tolist()},
+            'exchange': exchange,
+            'degraded': degraded,
             'roofline': roofline,
             'cpu_baseline': cpu,
             'end_to_end': e2e if rank == 0 and not sharded else None,
         }
         print(json.dumps(line), flush=True)
     if sharded:
+        dist.destroy_process_group()
+
+
+def main_ranks(args):
+    """Launcher check without a GPU: every rank joins a gloo group and contributes its rank; rank 0
+    prints the group size and the rank sum (tests/test_bench_launch.py)."""
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', 1))
+    rank = int(os.environ.get('RANK', 0))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        dist.init_process_group('gloo')
+    t = torch.tensor([rank], dtype=torch.int64)
+    if world > 1:
+        dist.all_reduce(t)
+    if rank == 0:
+        print(json.dumps({'workload': 'ranks', 'n_gpus': world, 'rank_sum': int(t.item())}), flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 
@@ -454,7 +531,7 @@ def main_ksd(args):
         c1.record(stream)
     e1.record(stream)
     torch.cuda.synchronize()
-    colsum_s = float(np.mean([c0.elapsed_time(c1) * 1e-3 for c0, c1 in ce]))
+    colsum_s = float(np.median([c0.elapsed_time(c1) * 1e-3 for c0, c1 in ce]))
     # full steps (column sums + all-reduce + finish)
     torch.cuda.synchronize()
     if world > 1:
@@ -470,7 +547,8 @@ def main_ksd(args):
     pairs = n * (n - 1) / 2
     rank_pairs = sum(n - 1 - a for a in range(a0, a1)) if n < 10 ** 4 else \
         (a1 - a0) * (n - 1) - (a1 * (a1 - 1) - a0 * (a0 - 1)) // 2
-    flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0) + 1     # + the column accumulate
+    flop_per_pair = algorithmic_flop_per_pair(d, gf) + 1     # + the column accumulate
+    isa_flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0) + 1
     if rank == 0:
         tflops = rank_pairs * flop_per_pair / colsum_s / 1e12
         line = {
@@ -486,7 +564,10 @@ def main_ksd(args):
             'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
                          'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': None,
                          'kernel': f'ksd_colsum_kernel<{d},{str(gf).lower()}>', 'kernel_avg_us': round(colsum_s * 1e6, 1),
-                         'flop_per_pair': flop_per_pair},
+                         'flop_per_pair': flop_per_pair,
+                         'flop_per_pair_source': 'SURVEY.md 8(d): 12 d + 40 (+2 gradient-free) + 1 accumulate',
+                         'issue': {'isa_flop_per_pair': isa_flop_per_pair,
+                                   'achieved_TFs': round(rank_pairs * isa_flop_per_pair / colsum_s / 1e12, 2)}},
         }
         print(json.dumps(line), flush=True)
     if world > 1:
@@ -684,4 +765,4 @@ def main_lv(args):
 
 
 if __name__ == '__main__':
-    main()
+    sys.exit(main() or 0)

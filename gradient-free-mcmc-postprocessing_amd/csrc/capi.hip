@@ -260,6 +260,32 @@ int st_greedy_sharded(const double* x_soa, const double* g_soa, const double* we
     return hip_check(e, "multi-rank persistent launch");
 }
 
+int st_greedy_sharded_supported(int64_t n, int32_t d, int32_t has_weights, int64_t row_begin,
+                                int64_t row_end, int32_t rank, int32_t nranks, int64_t n_points) {
+    if (d < 1 || d > st::kMaxDim || n < 1 || n_points < 1)
+        return fail(ST_ERR_INVALID, "bad problem (n = %lld, d = %d)", (long long)n, d);
+    if (nranks < 2 || nranks > st::kMailboxRanks || rank < 0 || rank >= nranks)
+        return fail(ST_ERR_INVALID, "bad rank %d of %d", rank, nranks);
+    if (row_begin < 0 || row_end <= row_begin || row_end > n)
+        return fail(ST_ERR_INVALID, "need 0 <= row_begin < row_end <= n");
+    // the same decision st_greedy_sharded takes, without touching any buffer: placeholders for the
+    // pointers, a non-null inbox, the workspace size the caller allocates (st_greedy_workspace_bytes)
+    static uint64_t dummy_box[2];
+    st::RankSpec rs{};
+    rs.row_begin = row_begin;
+    rs.row_end = row_end;
+    rs.rank = rank;
+    rs.nranks = nranks;
+    rs.inbox = dummy_box;
+    static double dummy_w;
+    int used = 0;
+    const hipError_t e = st::launch_greedy_persistent(
+        nullptr, nullptr, has_weights ? &dummy_w : nullptr, nullptr, n, d, 0, 1.0, 1.0, n_points, nullptr,
+        nullptr, greedy_ws_bytes(d), nullptr, &used, &rs, true);
+    if (e == hipErrorInvalidValue) return fail(ST_ERR_INVALID, "invalid shard");
+    return used ? 1 : 0;
+}
+
 int st_greedy_step(const double* x_soa, const double* g_soa, const double* weights, int64_t n,
                    int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t row_offset,
                    int64_t t, int32_t nranks, const double* cands_in, double* cand_out,

@@ -889,7 +889,7 @@ static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
-                                    int* used, const RankSpec* rs) {
+                                    int* used, const RankSpec* rs, bool plan_only) {
     *used = 0;
     const RankSpec one{0, n, 0, 1, 0, nullptr, {}};
     if (!rs) rs = &one;
@@ -952,6 +952,10 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     const size_t lds = wide ? head + (size_t)d * 256 * sizeof(double) : head + (size_t)RL * row_bytes;
     if (wide && lds > (size_t)(lds_max > 0 ? lds_max : 65536)) return hipErrorNotSupported;
 
+    if (plan_only) {   // eligibility query (st_greedy_sharded_supported): everything but the launch
+        *used = 1;
+        return hipSuccess;
+    }
     char* p = static_cast<char*>(ws);
     PersistArgs a{};
     a.x = x; a.g = g; a.w = w; a.A = A;

@@ -66,7 +66,7 @@ int64_t persistent_ws_bytes(int d, int G, int rec_stride);
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
-                                    int* used, const RankSpec* ranks = nullptr);
+                                    int* used, const RankSpec* ranks = nullptr, bool plan_only = false);
 hipError_t launch_mailbox_handshake(const MailboxPeers& peers, uint64_t* inbox, int rank,
                                     int nranks, uint64_t token, int* ok, hipStream_t s);
 hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStream_t s);

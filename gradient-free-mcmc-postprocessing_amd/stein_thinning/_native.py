@@ -70,6 +70,7 @@ SIGNATURES = {
     'st_greedy_sharded': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
                                          _i64, _i64, _i32, _i32, _c_dp, ctypes.c_uint64, _i64,
                                          _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
+    'st_greedy_sharded_supported': (ctypes.c_int, [_i64, _i32, _i32, _i64, _i64, _i32, _i32, _i64]),
     'st_greedy_step_exchange': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
                                                _i64, _i64, _i32, _i32, _c_dp, _c_dp, _c_dp, _c_dp,
                                                _c_dp, _i64, _c_dp, _c_dp]),

@@ -344,6 +344,18 @@ def exchange_engine(d: int, world: int, n: Optional[int] = None) -> str:
     return 'steps'
 
 
+def persistent_supported(integrand: SteinIntegrand, rank: int, world: int, n_points: int,
+                         group=None) -> bool:
+    """Group-wide verdict of the C launcher's own eligibility check (st_greedy_sharded_supported:
+    d, rows per block against the kernel's register / LDS budget, the grid cap) for every rank's
+    block -- exchange_engine's choice is a cheap pre-filter, this is the launcher's decision."""
+    r0, r1 = shard_bounds(integrand.n, rank, world)
+    rc = nat.lib().st_greedy_sharded_supported(integrand.n, integrand.sample.shape[1],
+                                               0 if integrand.weights is None else 1, r0, r1, rank, world,
+                                               int(n_points))
+    return _group_all(rc == 1, group)
+
+
 def device_exchange_eligible(d: int, world: int) -> bool:
     """Whether a mailbox (device-side) exchange engine serves this run."""
     return exchange_engine(d, world) != 'rccl'
@@ -558,10 +570,19 @@ def sharded_runner(integrand: SteinIntegrand, n_points: int, group=None, use_gra
     sample; indices compared across ranks), otherwise -- or if that disagrees -- to the RCCL
     record all-gather.  ``runner.mode`` names the engine; ``runner.launch()`` enqueues a further
     run."""
+    rank, world = _world(group)
+    engine = exchange_engine(integrand.sample.shape[1], world, integrand.n)
+    if engine == 'persistent' and not persistent_supported(integrand, rank, world, n_points, group):
+        engine = 'steps'   # e.g. d = 50 with more rows per block than the wide kernel holds
+    runner = _engine_runner(integrand, n_points, group, use_graph, engine)
+    runner.engine = engine   # the engine chosen; runner.mode names the one that ran
+    return runner
+
+
+def _engine_runner(integrand: SteinIntegrand, n_points: int, group, use_graph: bool, engine: str):
     import torch.distributed as dist
     rank, world = _world(group)
     d = integrand.sample.shape[1]
-    engine = exchange_engine(d, world, integrand.n)
     note = ''
     if engine == 'replicated':
         runner = ReplicatedGreedy(integrand, n_points)

@@ -145,6 +145,12 @@ int st_greedy_sharded(const double *x_soa, const double *g_soa, const double *we
                       void *const *peer_mailboxes, uint64_t seq_base, int64_t n_points,
                       uint32_t *idx_out, double *a_work, void *workspace,
                       int64_t workspace_bytes, void *stream);
+/* 1 if st_greedy_sharded would run this rank's block [row_begin, row_end) on the current device
+ * (the launcher's exact decision: d, rows per block against the kernel's register/LDS budget, the
+ * st_tune grid cap), 0 if it would return ST_ERR_UNSUPPORTED, < 0 on invalid arguments.  No GPU
+ * work; callers agree on it across ranks before choosing the engine. */
+int st_greedy_sharded_supported(int64_t n, int32_t d, int32_t has_weights, int64_t row_begin,
+                                int64_t row_end, int32_t rank, int32_t nranks, int64_t n_points);
 /*
  * Any d (the launch-per-step path of st_greedy_step) with the per-step rank exchange through the
  * same mailboxes instead of an RCCL all-gather: one call = the step kernel over this rank's shard

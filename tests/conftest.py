@@ -33,3 +33,21 @@ def curves():
 def gm():
     from oracle import models
     return models.gm_reference_sample()
+
+
+@pytest.fixture(scope='session')
+def config4():
+    """BASELINE config 4 (n = 2e6, d = 4, Langevin, 'med', m = 1000): raw LV-surrogate arrays, the
+    oracle's standardised inputs and the threaded C bit model's full 1000-step run on them
+    (oracle/stein_ref.c sr_greedy_mt: ~10 s on 16 host threads)."""
+    import numpy as np
+    from bench import lv_surrogate
+    from oracle import stein_numpy as o
+    from tests import oracle_c
+    n, m = 2_000_000, 1000
+    x, g, _, _ = lv_surrogate(n, 12345)
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'med')
+    l, tr = float(linv[0, 0]), float(np.trace(linv))
+    cidx, cA = oracle_c.greedy_mt(s, gs, None, l, tr, m)
+    return dict(x=x, g=g, s=s, gs=gs, l=l, tr=tr, m=m, idx=cidx, A=cA)

@@ -16,12 +16,15 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
             os.makedirs(os.path.dirname(LIB), exist_ok=True)
-            subprocess.run(['gcc', '-O2', '-fPIC', '-shared', '-ffp-contract=off', '-o', LIB, SRC, '-lm'],
+            subprocess.run(['gcc', '-O2', '-fPIC', '-shared', '-ffp-contract=off', '-pthread', '-o', LIB, SRC, '-lm'],
                            check=True)
         L = ctypes.CDLL(LIB)
         dp, i64 = ctypes.c_void_p, ctypes.c_int64
         L.sr_greedy.restype = ctypes.c_int
         L.sr_greedy.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp]
+        L.sr_greedy_mt.restype = ctypes.c_int
+        L.sr_greedy_mt.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp,
+                                   ctypes.c_int]
         L.sr_pairs.restype = ctypes.c_int
         L.sr_pairs.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, dp, i64, dp]
         _lib = L
@@ -41,6 +44,25 @@ def greedy(x, g, w, l, tr, m):
     idx = np.empty(m, dtype=np.uint32)
     A = np.empty(n, dtype=np.float64)
     rc = lib().sr_greedy(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A))
+    assert rc == 0
+    return idx, A
+
+
+def host_threads():
+    """Threads for the checker: the box's CPU share (OMP_NUM_THREADS is 16 on the GPU box, while
+    os.cpu_count() there reports the whole machine)."""
+    return max(1, min(int(os.environ.get('OMP_NUM_THREADS', 0)) or (os.cpu_count() or 1), 16))
+
+
+def greedy_mt(x, g, w, l, tr, m, nthreads=None):
+    """sr_greedy over row blocks on host threads: same indices and bit-identical A as greedy()."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    g = np.ascontiguousarray(g, dtype=np.float64)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    n, d = x.shape
+    idx = np.empty(m, dtype=np.uint32)
+    A = np.empty(n, dtype=np.float64)
+    rc = lib().sr_greedy_mt(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A), nthreads or host_threads())
     assert rc == 0
     return idx, A
 

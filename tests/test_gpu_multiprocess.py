@@ -203,3 +203,56 @@ def test_device_exchange_512_thread_shards_share_one_gpu(tmp_path):
     for r in range(world):
         assert (tmp_path / f'mode{r}.txt').read_text() == 'device-exchange'
         np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}.npy'), want)
+
+
+def _config4_worker(rank, world, port, out_dir, data_path, m):
+    """One of `world` ranks of config 4 on the shared GPU, grid 256 / world blocks each (bench.py's
+    rehearsal mode): the raw host arrays go through thin_sharded exactly as on one GPU per rank."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from stein_thinning import _native as nat
+        from stein_thinning import distributed as sd
+        assert nat.lib().st_tune(5, 256 // world) == 0
+        data = np.load(data_path)
+        idx = sd.thin_sharded(data['x'], data['g'], m, preconditioner='med')
+        np.save(os.path.join(out_dir, f'c4idx{rank}.npy'), idx)
+        with open(os.path.join(out_dir, f'c4mode{rank}.txt'), 'w') as f:
+            f.write(str(sd.last_mode))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config4_eight_ranks_share_one_gpu(tmp_path, config4):
+    """Config 4 (n = 2e6, m = 1000) split over 8 ranks as on an 8-GPU node (2.5e5 rows per rank),
+    the 8 processes sharing the one visible GPU with 32 blocks each: all 1000 indices identical to
+    the C bit model on every rank, through the in-kernel mailbox exchange."""
+    world = 8
+    data_path = str(tmp_path / 'c4.npz')
+    np.savez(data_path, x=config4['x'], g=config4['g'])
+    mp.spawn(_config4_worker, args=(world, _free_port(), str(tmp_path), data_path, config4['m']),
+             nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f'c4mode{r}.txt').read_text() == 'device-exchange'
+        np.testing.assert_array_equal(np.load(tmp_path / f'c4idx{r}.npy'), config4['idx'])
+
+
+def test_sharded_supported_query_matches_launcher():
+    """st_greedy_sharded_supported evaluates the persistent launcher's own eligibility: d = 2, 4 any
+    shard; d = 50 only while a rank's block has at most 256 rows (so the grid cap st_tune key 5
+    matters: config 5 at 8 ranks with 32 blocks per rank does NOT fit); other d never."""
+    from stein_thinning import _native as nat
+    L = nat.lib()
+    cus = torch.cuda.get_device_properties(0).multi_processor_count
+    n = 500_000
+    assert L.st_greedy_sharded_supported(2_000_000, 4, 0, 0, 250_000, 0, 8, 1000) == 1
+    assert L.st_greedy_sharded_supported(n, 50, 1, 0, n // 8, 0, 8, 500) == (1 if n // 8 <= 256 * cus else 0)
+    assert L.st_greedy_sharded_supported(n, 9, 1, 0, n // 8, 0, 8, 500) == 0
+    assert L.st_tune(5, 32) == 0
+    try:
+        assert L.st_greedy_sharded_supported(n, 50, 1, 0, n // 8, 0, 8, 500) == 0
+        assert L.st_greedy_sharded_supported(2_000_000, 4, 0, 0, 250_000, 0, 8, 1000) == 1
+    finally:
+        L.st_tune(5, -1)
+    assert L.st_greedy_sharded_supported(n, 50, 1, 10, 5, 0, 8, 500) < 0

@@ -366,32 +366,46 @@ def test_config5_d50_prefix():
                                       o.thin_gf(x, log_p, log_q, gq, 40, preconditioner='med'))
 
 
-def test_config4_full_size_properties():
-    """n = 2e6, m = 1000 (the headline workload): the 20-step prefix equals the oracle, and the final
-    running sums equal diag + 2 sum_t k(., x_idx[t]) bit for bit on sampled rows; the last index is
-    the argmin of the final sums."""
-    n, m = 2_000_000, 1000
-    x, g, _, _ = _lv_surrogate(n, 12345)
+def _oracle_inputs(x, g, log_p=None, log_q=None):
+    """The C bit model's inputs built by the NumPy oracle's own host steps (standardisation, 'med'
+    preconditioner, min-anchored weights: oracle/stein_numpy.py)."""
     s, gs = o._validate_and_standardize(x, g, True)
     linv = o.make_precon(s, 'med')
-    l, tr = linv[0, 0], np.trace(linv)
-    prob = DeviceProblem(s, gs, None, l, tr)
-    idx20 = prob.greedy(20)
-    np.testing.assert_array_equal(idx20, o.thin(x, g, 20, preconditioner='med'))
-    idx, A = prob.greedy(m, return_sums=True)
-    np.testing.assert_array_equal(idx[:20], idx20)
-    assert idx.max() < n
-    assert int(np.argmin(A)) == int(idx[-1]) or A[int(np.argmin(A))] == A[int(idx[-1])]
-    rows = np.unique(np.concatenate([np.random.default_rng(0).integers(0, n, 1500), idx[-5:].astype(np.int64)]))
-    xs, gss = s[rows], gs[rows]
-    ar = np.arange(rows.shape[0])
-    acc = oracle_c.pairs(xs, gss, None, l, tr, ar, ar)
-    for t in range(m - 1):
-        j = int(idx[t])
-        xx = np.vstack([xs, s[j][None]])
-        gg = np.vstack([gss, gs[j][None]])
-        acc = acc + 2.0 * oracle_c.pairs(xx, gg, None, l, tr, ar, np.full(ar.shape[0], ar.shape[0]))
-    assert np.array_equal(A[rows], acc)
+    w = None if log_p is None else np.exp(o._log_weights(log_p, log_q, None))
+    return s, gs, w, float(linv[0, 0]), float(np.trace(linv))
+
+
+def test_config4_full_length_bit_exact(config4):
+    """The headline workload, every step: all 1000 indices identical to the C bit model and the
+    final running sums bit-identical on all 2e6 rows; the bit model's first 20 indices identical to
+    the NumPy restatement of JAX_Stein_Thinning.ipynb:281-295 on the same input; the drop-in
+    thin() on host arrays returns the same indices."""
+    c = config4
+    np.testing.assert_array_equal(c['idx'][:20], o.thin(c['x'], c['g'], 20, preconditioner='med'))
+    prob = DeviceProblem(c['s'], c['gs'], None, c['l'], c['tr'])
+    idx, A = prob.greedy(c['m'], return_sums=True)
+    np.testing.assert_array_equal(idx, c['idx'])
+    assert np.array_equal(A, c['A']), np.flatnonzero(A != c['A'])[:10]
+    np.testing.assert_array_equal(st.thin(c['x'], c['g'], c['m'], preconditioner='med'), c['idx'])
+
+
+def test_config5_full_length_bit_exact():
+    """BASELINE config 5 at full size (n = 5e5, d = 50, gradient-free, m = 500 -- the launch-per-step
+    greedy_step_rt kernel on one GPU): all 500 indices identical to the C bit model, running sums
+    bit-identical; the bit model's first 5 indices identical to the NumPy restatement."""
+    from bench import gaussian_d50
+    m = 500
+    x, log_p, log_q, gq = gaussian_d50(500_000, 12349)
+    s, gs, w, l, tr = _oracle_inputs(x, gq, log_p, log_q)
+    cidx, cA = oracle_c.greedy_mt(s, gs, w, l, tr, m)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        np.testing.assert_array_equal(cidx[:5], o.thin_gf(x, log_p, log_q, gq, 5, preconditioner='med'))
+        integ = st._make_stein_gf_integrand(x, log_p, log_q, gq, preconditioner='med')
+    idx, A = integ.device_problem().greedy(m, return_sums=True)
+    np.testing.assert_array_equal(idx, cidx)
+    assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
+    np.testing.assert_array_equal(st._greedy_search(m, integ), cidx)
 
 
 def test_two_shards_on_one_gpu_equal_single():

@@ -115,3 +115,28 @@ def test_c_model_greedy_matches_numpy_oracle(d, pre, gf):
     linv = o.make_precon(s, pre)
     idx, _ = oracle_c.greedy(s, gs, w, linv[0, 0], np.trace(linv), m)
     np.testing.assert_array_equal(idx, want)
+
+
+@pytest.mark.parametrize('d,gf', [(2, True), (4, False), (9, False), (50, True)])
+def test_threaded_bit_model_equals_sequential(d, gf):
+    """sr_greedy_mt (the checker of the full-size GPU tests) equals sr_greedy for any thread count:
+    same indices (lowest index among exact ties across thread blocks, first NaN) and bit-identical
+    running sums."""
+    from tests import oracle_c
+    rng = np.random.default_rng(d)
+    n, m = 3_001, 40
+    x = rng.normal(size=(n, d))
+    x[2_000:2_200] = x[10:210]                 # exact ties across thread-block boundaries
+    g = -x + 0.1 * rng.normal(size=(n, d))
+    g[2_000:2_200] = g[10:210]
+    w = None
+    if gf:
+        lw = rng.normal(size=n)
+        lw[[7, 2_500]] = 800.0                   # exp overflow -> inf weights -> NaN sums
+        with np.errstate(over='ignore'):
+            w = np.exp(lw - lw.min())
+    want_idx, want_A = oracle_c.greedy(x, g, w, 0.7, 0.7 * d, m)
+    for nt in (1, 2, 3, 7, 16):
+        idx, A = oracle_c.greedy_mt(x, g, w, 0.7, 0.7 * d, m, nt)
+        np.testing.assert_array_equal(idx, want_idx)
+        assert np.array_equal(A, want_A, equal_nan=True)
