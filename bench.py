@@ -133,11 +133,21 @@ def make_integrand(cfg):
     return st._make_stein_integrand(x, g, preconditioner='med'), x, g
 
 
-def cpu_baseline(cfg, integrand, steps: int):
-    """The NumPy restatement of the reference path (oracle/stein_numpy.py) on the same standardised
-    input, diagonal + `steps` greedy steps, timed on this host (NumPy ufuncs: 1 core)."""
+def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None):
+    """Host baselines on the same standardised input (test-infrastructure code, timed only):
+    * primary: the C restatement (oracle/stein_ref.c sr_greedy_mt -- the kernels' bit model, rows
+      split over host threads like the reference's process fan-out, code/src/utils/parallel.py:48-52)
+      running the FULL m-step thin on the box's CPU share; its indices are compared with the GPU's;
+    * `numpy_1core`: the NumPy restatement of the reference path (oracle/stein_numpy.py: the
+      (d, n) transposed vfk0_imq, A += 2 col, np.argmin) for the diagonal + `steps` steps on one
+      core (NumPy ufuncs are single-threaded), extrapolated to m."""
     from oracle import stein_numpy as ref
+    from oracle import stein_ref_c
     s, g, w = integrand.sample, integrand.gradient, integrand.weights
+    nt = stein_ref_c.host_threads()
+    t0 = time.perf_counter()
+    cidx, _ = stein_ref_c.greedy_mt(s, g, w, integrand.linv_scale, integrand.linv_trace, cfg['m'], nt)
+    dt_c = time.perf_counter() - t0
     vfk0 = ref.make_imq(s, 'med')
     if w is None:
         def f(i1, i2):
@@ -149,12 +159,17 @@ def cpu_baseline(cfg, integrand, steps: int):
     ref._greedy_search(steps + 1, f)
     dt = time.perf_counter() - t0
     pairs = cfg['n'] * (steps + 1)
-    return {'value': pairs / dt, 'unit': 'pair-evals/s', 'cores': 1, 'kind': 'port',
-            'sample': (f"oracle.stein_numpy._greedy_search (NumPy restatement of the reference path) on the "
-                       f"same standardised input, n={cfg['n']}, diagonal + {steps} steps = {pairs:.3g} pair-evals "
-                       f"in {dt:.1f} s; full m={cfg['m']} thin extrapolated: {cfg['n'] * cfg['m'] * dt / pairs:.0f} s; "
-                       f"NumPy {np.__version__}, single-threaded ufuncs, host {platform.processor() or platform.machine()} "
-                       f"({os.cpu_count()} logical CPUs)")}
+    full = cfg['n'] * cfg['m']
+    host = f"{platform.processor() or platform.machine()} ({os.cpu_count()} logical CPUs visible)"
+    return {'value': full / dt_c, 'unit': 'pair-evals/s', 'cores': nt, 'kind': 'port',
+            'sample': (f"oracle/stein_ref.c sr_greedy_mt (C restatement of the reference greedy loop, "
+                       f"JAX_Stein_Thinning.ipynb:281-295, bit model of the kernels) on {nt} host threads: the full "
+                       f"n={cfg['n']}, m={cfg['m']} thin ({full:.3g} pair-evals) in {dt_c:.1f} s; host {host}"),
+            'same_indices_as_gpu': None if gpu_idx is None else bool(np.array_equal(cidx, gpu_idx)),
+            'numpy_1core': {'value': pairs / dt, 'unit': 'pair-evals/s', 'cores': 1,
+                            'sample': (f"oracle.stein_numpy._greedy_search (NumPy restatement of the reference "
+                                       f"path), diagonal + {steps} steps = {pairs:.3g} pair-evals in {dt:.1f} s; "
+                                       f"full thin extrapolated {full * dt / pairs:.0f} s; NumPy {np.__version__}")}}
 
 
 def kernel_timing(prob, n_points: int, repeats: int = 5):
@@ -254,7 +269,7 @@ def main():
     ap.add_argument('--steps', type=int, default=5, help='timed thins')
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
-    ap.add_argument('--cpu-steps', type=int, default=60, help='greedy steps of the CPU baseline sample')
+    ap.add_argument('--cpu-steps', type=int, default=30, help='greedy steps of the NumPy one-core sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
     ap.add_argument('--no-graph', action='store_true', help='N > 1: eager per-step launches instead of a HIP graph')
@@ -412,7 +427,7 @@ def main():
                             'bytes_per_pair': bytes_per_pair,
                             'timing': 'HIP events around back-to-back single-step launches'}
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(cfg, integrand, args.cpu_steps)
+            cpu = cpu_baseline(cfg, integrand, args.cpu_steps, result_idx)
         e2e = None
         if world == 1 and not cfg['gf'] and not cfg.get('d50'):
             # the drop-in call on host arrays (not `value`): standardisation + 'med' + H2D upload +
@@ -421,9 +436,9 @@ def main():
             st.thin(host_x, host_g, m, preconditioner='med')
             t_e = time.perf_counter()
             e2e_idx = st.thin(host_x, host_g, m, preconditioner='med')
-            e2e = {'thin_host_arrays_s': round(time.perf_counter() - t_e, 4),
-                   'pair_evals_per_s': n * m / (time.perf_counter() - t_e),
-                   'same_indices': bool(np.array_equal(e2e_idx, result_idx))}
+            dt_e = time.perf_counter() - t_e
+            e2e = {'thin_host_arrays_s': round(dt_e, 4), 'pair_evals_per_s': n * m / dt_e,
+                   'same_indices_as_timed_run': bool(np.array_equal(e2e_idx, result_idx))}
 
     exchange, degraded = None, False
     if sharded:

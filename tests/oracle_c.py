@@ -1,79 +1,2 @@
-"""ctypes loader for the C bit-model oracle (oracle/stein_ref.c) -- test infrastructure."""
-import ctypes
-import os
-import subprocess
-
-import numpy as np
-
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB = os.path.join(ROOT, 'oracle', '_build', 'libstein_ref.so')
-SRC = os.path.join(ROOT, 'oracle', 'stein_ref.c')
-_lib = None
-
-
-def lib():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(SRC):
-            os.makedirs(os.path.dirname(LIB), exist_ok=True)
-            subprocess.run(['gcc', '-O2', '-fPIC', '-shared', '-ffp-contract=off', '-pthread', '-o', LIB, SRC, '-lm'],
-                           check=True)
-        L = ctypes.CDLL(LIB)
-        dp, i64 = ctypes.c_void_p, ctypes.c_int64
-        L.sr_greedy.restype = ctypes.c_int
-        L.sr_greedy.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp]
-        L.sr_greedy_mt.restype = ctypes.c_int
-        L.sr_greedy_mt.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp,
-                                   ctypes.c_int]
-        L.sr_pairs.restype = ctypes.c_int
-        L.sr_pairs.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, dp, i64, dp]
-        _lib = L
-    return _lib
-
-
-def _p(a):
-    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
-
-
-def greedy(x, g, w, l, tr, m):
-    """Bit-model greedy run: returns (idx uint32, running sums A)."""
-    x = np.ascontiguousarray(x, dtype=np.float64)
-    g = np.ascontiguousarray(g, dtype=np.float64)
-    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
-    n, d = x.shape
-    idx = np.empty(m, dtype=np.uint32)
-    A = np.empty(n, dtype=np.float64)
-    rc = lib().sr_greedy(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A))
-    assert rc == 0
-    return idx, A
-
-
-def host_threads():
-    """Threads for the checker: the box's CPU share (OMP_NUM_THREADS is 16 on the GPU box, while
-    os.cpu_count() there reports the whole machine)."""
-    return max(1, min(int(os.environ.get('OMP_NUM_THREADS', 0)) or (os.cpu_count() or 1), 16))
-
-
-def greedy_mt(x, g, w, l, tr, m, nthreads=None):
-    """sr_greedy over row blocks on host threads: same indices and bit-identical A as greedy()."""
-    x = np.ascontiguousarray(x, dtype=np.float64)
-    g = np.ascontiguousarray(g, dtype=np.float64)
-    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
-    n, d = x.shape
-    idx = np.empty(m, dtype=np.uint32)
-    A = np.empty(n, dtype=np.float64)
-    rc = lib().sr_greedy_mt(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A), nthreads or host_threads())
-    assert rc == 0
-    return idx, A
-
-
-def pairs(x, g, w, l, tr, i1, i2):
-    x = np.ascontiguousarray(x, dtype=np.float64)
-    g = np.ascontiguousarray(g, dtype=np.float64)
-    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
-    i1 = np.ascontiguousarray(i1, dtype=np.int64)
-    i2 = np.ascontiguousarray(i2, dtype=np.int64)
-    out = np.empty(i1.shape[0], dtype=np.float64)
-    rc = lib().sr_pairs(_p(x), _p(g), _p(w), x.shape[0], x.shape[1], l, tr, _p(i1), _p(i2), i1.shape[0], _p(out))
-    assert rc == 0
-    return out
+"""The C bit-model checker (oracle/stein_ref_c.py), under the name the tests import."""
+from oracle.stein_ref_c import greedy, greedy_mt, host_threads, lib, pairs  # noqa: F401
