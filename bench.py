@@ -779,5 +779,16 @@ def main_lv(args):
         dist.destroy_process_group()
 
 
+def _dump_maps():
+    """ST_BENCH_DUMP_MAPS=<file>: the process's memory map at the end of main (resolves the
+    addresses of a crash in exit-time destructors)."""
+    path = os.environ.get('ST_BENCH_DUMP_MAPS')
+    if path:
+        with open('/proc/self/maps') as src, open(path, 'w') as dst:
+            dst.write(src.read())
+
+
 if __name__ == '__main__':
-    sys.exit(main() or 0)
+    rc = main() or 0
+    _dump_maps()
+    sys.exit(rc)

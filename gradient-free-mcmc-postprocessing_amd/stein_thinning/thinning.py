@@ -18,6 +18,7 @@ and the argmins run in HIP kernels on the GPU (``_native`` C-ABI).  Integrands b
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import warnings
 from typing import Callable, Optional
@@ -132,6 +133,9 @@ class SteinIntegrand:
 
     ``integrand(ind1, ind2)`` returns k(x[ind1], x[ind2]) (times w[ind1] w[ind2] for the
     gradient-free kernel), broadcasting ind1 against ind2 like the reference's NumPy integrand.
+    ``reindex(rows)`` is the view ``(a, b) -> integrand(rows[a], rows[b])`` -- what the reference
+    harness's ``reindex_integrand`` closure computes (``code/src/utils/ksd.py:9-16``) -- sharing
+    this integrand's device arrays; ``thin`` / ``stein.ksd`` / ``stein.kmat`` accept it directly.
     """
 
     def __init__(self, sample: np.ndarray, gradient: np.ndarray, linv: np.ndarray,
@@ -146,26 +150,67 @@ class SteinIntegrand:
             raise NotImplementedError('only isotropic preconditioners run on the HIP engine')
         self.linv_scale, self.linv_trace = iso
         self._problem = None
+        self._base: Optional['SteinIntegrand'] = None   # views: the integrand whose rows these index
+        self._rows: Optional[np.ndarray] = None
+        self._rec = None
 
     @property
     def n(self) -> int:
-        return self.sample.shape[0]
+        return self.sample.shape[0] if self._rows is None else self._rows.shape[0]
+
+    def reindex(self, indices) -> 'SteinIntegrand':
+        """View over rows ``indices`` of this integrand (no copy of the device arrays)."""
+        view = SteinIntegrand.__new__(SteinIntegrand)
+        view.__dict__.update(self.__dict__)
+        view._problem = None
+        view._rec = None
+        view._base = self.base()
+        view._rows = self.base_rows(np.asarray(indices, dtype=np.int64).reshape(-1))
+        return view
+
+    def base(self) -> 'SteinIntegrand':
+        return self if self._base is None else self._base
+
+    def base_rows(self, rows) -> np.ndarray:
+        """Rows of the base integrand that this integrand's indices ``rows`` denote."""
+        local = np.arange(self.n)[rows]   # reference indexing semantics (negative wrap, IndexError)
+        return local if self._rows is None else self._rows[local]
+
+    def base_problem(self):
+        return self.base().device_problem()
 
     def device_problem(self):
         if self._problem is None:
-            from .device import DeviceProblem
-            self._problem = DeviceProblem(self.sample, self.gradient, self.weights,
-                                          self.linv_scale, self.linv_trace)
+            if self._base is not None:
+                self._problem = self._base.device_problem().subset(self._rows)
+            else:
+                from .device import DeviceProblem
+                self._problem = DeviceProblem(self.sample, self.gradient, self.weights,
+                                              self.linv_scale, self.linv_trace)
         return self._problem
 
-    def _index(self, ind) -> np.ndarray:
-        return np.arange(self.n)[ind]
+    @contextlib.contextmanager
+    def recording(self):
+        """Trace mode for stein.ksd / kmat dispatch: calls record their (broadcast) index arrays
+        and return signed pair-specific sentinel values instead of evaluating (no GPU work)."""
+        self._rec = []
+        try:
+            yield self._rec
+        finally:
+            self._rec = None
 
     def __call__(self, ind1, ind2) -> np.ndarray:
-        i1 = np.atleast_1d(self._index(ind1))
-        i2 = np.atleast_1d(self._index(ind2))
+        i1 = np.atleast_1d(np.arange(self.n)[ind1])
+        i2 = np.atleast_1d(np.arange(self.n)[ind2])
         b1, b2 = np.broadcast_arrays(i1, i2)
-        out = self.device_problem().pairs(b1.reshape(-1), b2.reshape(-1))
+        if self._rec is not None:
+            u1, u2 = b1.astype(np.int64), b2.astype(np.int64)
+            sent = (((u1 * 2654435761 + u2 * 40503) % 1000003) + 0.375) * np.where((u1 + u2) % 2 == 0, 1.0, -1.0)
+            self._rec.append((np.array(b1), np.array(b2), sent))
+            return sent.copy()
+        r1 = self.base_rows(b1.reshape(-1))
+        r2 = self.base_rows(b2.reshape(-1))
+        out = self.base_problem().pairs(r1, r2)
         return out.reshape(b1.shape)
 
 

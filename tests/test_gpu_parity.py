@@ -428,3 +428,53 @@ def test_two_shards_on_one_gpu_equal_single():
         be.finalize(m - 1)
         np.testing.assert_array_equal(be.indices(), want)
     np.testing.assert_array_equal(want, o.thin(x, g, m, preconditioner='med'))
+
+
+def test_ksd_kmat_wrappers_run_one_device_launch(gm_gpu, monkeypatch):
+    """stein.ksd / kmat on wrappers of a SteinIntegrand under any name (closure, lambda, callable
+    object, functools.partial, the reindex view): ONE tiled-KSD / kmat launch and no pair-kernel
+    launch, values as calculate_ksd's (code/src/utils/ksd.py:19-27);
+    a wrapper with arithmetic of its own runs the batched protocol (no per-row launches)."""
+    import functools
+    from stein_thinning.device import DeviceProblem
+    calls = {'ksd': 0, 'kmat': 0, 'pairs': 0}
+    for name in calls:
+        orig = getattr(DeviceProblem, name)
+
+        def counted(self, *a, _orig=orig, _name=name, **k):
+            calls[_name] += 1
+            return _orig(self, *a, **k)
+        monkeypatch.setattr(DeviceProblem, name, counted)
+    idx = gm_gpu['idx_st']
+    integ = st._make_stein_integrand(gm_gpu['sample'], gm_gpu['gradient'])
+    want = o.calculate_ksd(gm_gpu['sample'], gm_gpu['gradient'], idx)
+
+    class Reindexed:
+        def __init__(self, f, rows):
+            self.f, self.rows = f, rows
+
+        def __call__(self, i, j):
+            return self.f(self.rows[i], self.rows[j])
+
+    def take(rows, f, i, j):
+        return f(rows[i], rows[j])
+    m = idx.shape[0]
+    for w in [lambda i, j: integ(idx[i], idx[j]), Reindexed(integ, idx), functools.partial(take, idx, integ),
+              integ.reindex(idx)]:
+        for k in calls:
+            calls[k] = 0
+        ks = ss.ksd(w, m)
+        np.testing.assert_allclose(ks, want, rtol=1e-10)
+        assert calls['ksd'] == 1 and calls['pairs'] == 0, calls
+    for k in calls:
+        calls[k] = 0
+    km = ss.kmat(Reindexed(integ, idx[:300]), 300)
+    assert calls['kmat'] == 1 and calls['pairs'] == 0, calls
+    np.testing.assert_array_equal(km, ss.kmat(integ.reindex(idx[:300]), 300))
+    # a wrapper doing its own arithmetic: the batched protocol, values as the reference loop's
+    for k in calls:
+        calls[k] = 0
+    scaled = ss.ksd(lambda i, j: 0.5 * integ(idx[i], idx[j]), 200)
+    assert calls['ksd'] == 0 and calls['pairs'] == 1, calls
+    ref_int = o._make_stein_integrand(gm_gpu['sample'], gm_gpu['gradient'])
+    np.testing.assert_allclose(scaled, o.ksd(lambda i, j: 0.5 * ref_int(idx[i], idx[j]), 200), rtol=1e-12)

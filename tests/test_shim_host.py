@@ -111,18 +111,49 @@ def test_protocol_ksd_with_user_integrand_matches_oracle(biv):
     np.testing.assert_allclose(ss.ksd(integrand, 50), o.ksd(integrand, 50), rtol=1e-12)
 
 
-def test_reindex_closure_is_recognised():
+def test_reindex_wrappers_are_traced_without_gpu():
+    """Any wrapper that reaches one SteinIntegrand -- the reference's reindex closure
+    (code/src/utils/ksd.py:9-16), a renamed closure, a lambda, functools.partial, a callable
+    object, the SteinIntegrand.reindex view -- yields its row map from one recorded call, with no
+    GPU work; wrappers that call the integrand twice or reach two integrands are not traced."""
+    import functools
     s = np.random.default_rng(0).normal(size=(20, 2))
     integ = st.SteinIntegrand(s, -s, np.identity(2))
-    idx = np.array([3, 1, 2])
+    other = st.SteinIntegrand(s, -s, np.identity(2))
+    idx = np.array([3, 1, 2, 19, 0])
 
     def reindex_integrand(integrand, indices):   # code/src/utils/ksd.py:9-16
         def res(ind1, ind2):
             return integrand(indices[ind1], indices[ind2])
         return res
-    got = ss._resolve(reindex_integrand(integ, idx))
-    assert got is not None and got[0] is integ and np.array_equal(got[1], idx)
-    assert ss._resolve(lambda a, b: a) is None
+
+    def make_view(f, rows):
+        def my_wrapper(i, j):
+            return f(rows[i], rows[j])
+        return my_wrapper
+
+    class Reindexed:
+        def __init__(self, f, rows):
+            self.f, self.rows = f, rows
+
+        def __call__(self, i, j):
+            return self.f(self.rows[i], self.rows[j])
+
+    def take(rows, f, i, j):
+        return f(rows[i], rows[j])
+
+    n = idx.shape[0]
+    for w in [reindex_integrand(integ, idx), make_view(integ, idx), lambda i, j: integ(idx[i], idx[j]),
+              Reindexed(integ, idx), functools.partial(take, idx, integ)]:
+        assert ss._inner_integrand(w) is integ
+        np.testing.assert_array_equal(ss._record_rows(w, integ, n), idx)
+    view = integ.reindex(idx)
+    assert view.n == n and view.base() is integ
+    np.testing.assert_array_equal(view.base_rows(np.arange(n)), idx)
+    np.testing.assert_array_equal(integ.reindex(idx).reindex([4, 0]).base_rows([0, 1]), [0, 3])
+    assert ss._record_rows(lambda i, j: integ(idx[i], idx[j]) + integ(idx[i], idx[j]), integ, n) is None
+    assert ss._inner_integrand(lambda i, j: integ(i, j) - other(i, j)) is None
+    assert ss._inner_integrand(lambda a, b: a) is None
 
 
 def test_device_path_refuses_without_gpu(biv):
