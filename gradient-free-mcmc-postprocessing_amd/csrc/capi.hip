@@ -141,7 +141,7 @@ int st_greedy(const double* x_soa, const double* g_soa, const double* weights, i
         x_soa, g_soa, weights, a_work, n, d, ld, linv_scale, linv_trace, n_points, idx_out, workspace,
         workspace_bytes, static_cast<hipStream_t>(stream), &used);
     if (used) return ST_OK;
-    if (pe != hipErrorNotSupported) (void)hipGetLastError();   // clear a failed cooperative launch
+    if (pe != hipErrorNotSupported) (void)hipGetLastError();   // clear a failed launch
     return st_greedy_steps(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, 0, n_points,
                            n_points, idx_out, a_work, workspace, workspace_bytes, stream);
 }

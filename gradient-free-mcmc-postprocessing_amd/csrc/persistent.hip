@@ -1,6 +1,6 @@
 // Persistent, on-chip-resident greedy kernel (K4) for gfx950.
 //
-// One cooperative launch runs the whole greedy loop of the reference's _greedy_search
+// One launch runs the whole greedy loop of the reference's _greedy_search
 // (JAX_Stein_Thinning.ipynb cell 22, json ~281-295; report.tex:413-426) for one device:
 //   * G <= #CU blocks of 256 threads, one per CU.  Block b owns rows [b*R, (b+1)*R).
 //   * Its rows live on chip for the whole run: RT rows per thread in VGPRs/AGPRs (x, g, A[, w]),
@@ -850,39 +850,54 @@ int persistent_tune(int key, int value) {
 }
 
 template <int D, bool GF, int RT, int NT, int BPC = 1>
-static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s) {
+static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s, bool dry) {
     auto fn = greedy_persistent<D, GF, RT, NT, BPC>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
+    // co-residency of the whole grid (every block spins on the others' records): checked here
+    // against the occupancy query -- what hipLaunchCooperativeKernel would check at launch -- and
+    // then a PLAIN launch of the same one-block-per-CU grid (same residency, MI355X_MICROARCH.md
+    // coop-launch row).  The cooperative path also made the HIP runtime create a cooperative queue
+    // whose exit-time teardown crashes when rocprofv3's tool has finalised HSA first
+    // (profiles/r02_exit_crash_bisect.log); a rank that cannot make progress times out, it never hangs.
+    int dev = 0, cus = 0, per_cu = 0;
+    if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), NT, lds)) !=
+        hipSuccess)
+        return e;
+    if ((int64_t)per_cu * cus < G) return hipErrorNotSupported;
+    if (dry) return hipSuccess;
     PersistArgs args = a;
     void* kargs[] = {&args};
-    // one device: cooperative launch (co-residency checked at launch).  Several ranks: a plain
-    // launch of the same one-block-per-CU grid (same residency, MI355X_MICROARCH.md coop-launch
-    // row), so that ranks sharing a device in tests are not serialised by the cooperative queue;
-    // a rank that cannot make progress times out, it never hangs.
-    if (a.nranks > 1)
-        return hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs, lds, s);
-    return hipLaunchCooperativeKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs,
-                                      lds, s);
+    return hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs, lds, s);
 }
 
 template <int D, bool GF>
-static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int G, size_t lds, hipStream_t s) {
+static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int G, size_t lds, hipStream_t s,
+                               bool dry) {
     if (bpc == 2) {
-        if (rt <= 4) return launch_p<D, GF, 4, 256, 2>(a, G, lds, s);
-        return launch_p<D, GF, 8, 256, 2>(a, G, lds, s);
+        if (rt <= 4) return launch_p<D, GF, 4, 256, 2>(a, G, lds, s, dry);
+        return launch_p<D, GF, 8, 256, 2>(a, G, lds, s, dry);
     }
     if (nt == 512) {
-        if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s);
-        if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s);
-        return launch_p<D, GF, 8, 512>(a, G, lds, s);
+        if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s, dry);
+        if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s, dry);
+        return launch_p<D, GF, 8, 512>(a, G, lds, s, dry);
     }
     switch (rt) {
-        case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s);
-        case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s);
-        default: return launch_p<D, GF, 16, 256>(a, G, lds, s);
+        case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s, dry);
+        case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s, dry);
+        default: return launch_p<D, GF, 16, 256>(a, G, lds, s, dry);
     }
+}
+
+static hipError_t launch_kind(const PersistArgs& a, int d, bool wide, bool gf, int rt, int nt, int bpc, int G,
+                              size_t lds, hipStream_t s, bool dry) {
+    if (wide) return gf ? launch_p<kWideD, true, 1, 256>(a, G, lds, s, dry) : launch_p<kWideD, false, 1, 256>(a, G, lds, s, dry);
+    if (d == 2) return gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s, dry) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s, dry);
+    return gf ? launch_p_rt<4, true>(a, rt, nt, bpc, G, lds, s, dry) : launch_p_rt<4, false>(a, rt, nt, bpc, G, lds, s, dry);
 }
 
 // Returns hipErrorNotSupported when the persistent path does not apply (caller falls back).
@@ -902,11 +917,9 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         (rs->nranks > 1 && !rs->inbox))
         return hipErrorInvalidValue;
     const int64_t n_shard = rs->row_end - rs->row_begin;
-    int dev = 0, cus = 0, lds_max = 0, lds_optin = 0, coop = 0;
+    int dev = 0, cus = 0, lds_max = 0, lds_optin = 0;
     if (hipGetDevice(&dev) != hipSuccess) return hipErrorNotSupported;
     if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        return hipErrorNotSupported;
-    if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev) != hipSuccess || !coop)
         return hipErrorNotSupported;
     if (hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, dev) != hipSuccess)
         return hipErrorNotSupported;
@@ -952,12 +965,13 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     const size_t lds = wide ? head + (size_t)d * 256 * sizeof(double) : head + (size_t)RL * row_bytes;
     if (wide && lds > (size_t)(lds_max > 0 ? lds_max : 65536)) return hipErrorNotSupported;
 
-    if (plan_only) {   // eligibility query (st_greedy_sharded_supported): everything but the launch
-        *used = 1;
-        return hipSuccess;
-    }
     char* p = static_cast<char*>(ws);
     PersistArgs a{};
+    if (plan_only) {   // eligibility query (st_greedy_sharded_supported): everything but the launch
+        hipError_t e = launch_kind(a, d, wide, gf, rt, nt, bpc, G, lds, s, true);
+        if (e == hipSuccess) *used = 1;
+        return e;
+    }
     a.x = x; a.g = g; a.w = w; a.A = A;
     a.n = n; a.ld = ld; a.l = l; a.tr = tr; a.m = m;
     a.idx_out = idx_out;
@@ -977,9 +991,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     // zero status and every granule tag (a stale tag from a previous run must never match)
     hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G, pitch), s);
     if (e != hipSuccess) return e;
-    if (wide) e = gf ? launch_p<kWideD, true, 1, 256>(a, G, lds, s) : launch_p<kWideD, false, 1, 256>(a, G, lds, s);
-    else if (d == 2) e = gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s);
-    else e = gf ? launch_p_rt<4, true>(a, rt, nt, bpc, G, lds, s) : launch_p_rt<4, false>(a, rt, nt, bpc, G, lds, s);
+    e = launch_kind(a, d, wide, gf, rt, nt, bpc, G, lds, s, false);
     if (e == hipSuccess) *used = 1;
     return e;
 }

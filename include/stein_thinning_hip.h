@@ -74,7 +74,8 @@ int64_t st_candidate_stride(int32_t d);
  * Whole greedy run on one device: idx_out[0..n_points) (device, uint32) receives the selected
  * row indices exactly as the reference's `thin` / `thin_gf` / `_greedy_search` return them;
  * a_work (ld doubles, device) ends holding the running sums A after the last step.
- * For d = 2 and 4 the run is ONE cooperative launch of the persistent on-chip-resident kernel
+ * For d = 2 and 4 the run is ONE launch of the persistent on-chip-resident kernel (grid checked
+ * against the occupancy query first)
  * (one block per CU; rows held in VGPRs/LDS across steps); if its internal bounded wait times
  * out, the unwritten entries of idx_out are set to UINT32_MAX (callers check idx < n).
  * Other d: one fused launch per step.
