@@ -276,6 +276,7 @@ def main():
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
+    ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
     ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'ranks'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
                          '(row-sharded, RCCL all-reduce of the n-length column-sum vector); ranks: launcher '
@@ -617,6 +618,7 @@ def main_proxy(args):
         c_log = psd.rank * proxy._LOG_2PI + psd.log_pdet
     r0, r1 = shard_bounds(n, rank, world)
     rows = r1 - r0
+    nat.check(nat.lib().st_tune(7, args.proxy_mode), 'st_tune')
     xd = torch.from_numpy(np.ascontiguousarray(x[r0:r1])).to(dev)
     loc = torch.from_numpy(mean).to(dev)
     U = torch.from_numpy(np.ascontiguousarray(psd.U)).to(dev)
@@ -643,7 +645,7 @@ def main_proxy(args):
         e1.record(stream)
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    kern_s = float(np.mean([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
+    kern_s = float(np.median([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
     if world > 1:
         dist.barrier()
         elapsed, kern_s = _max_over_ranks([elapsed, kern_s], dev)
@@ -651,7 +653,7 @@ def main_proxy(args):
         # algorithmic work of the kernel that runs: 16 < d <= 64 -> the matrix-core kernel (one
         # product y = P dev per row, Mahalanobis term dev . y: 2d^2 + 2d flop + the epilogue);
         # otherwise the VALU kernel (z = dev U and y: 4d^2 + 2d)
-        mfma = 16 < d <= 64
+        mfma = 16 < d <= 64 and args.proxy_mode != 1
         flop_row = (2 * d * d + 2 * d if mfma else 4 * d * d + 2 * d) + (2 * d + 12 if t_kind else 2)
         bytes_row = 16 * d + 8
         tflops = rows * flop_row / kern_s / 1e12
@@ -670,7 +672,11 @@ def main_proxy(args):
                   'frac': round(gbs / HBM_PEAK_GBS, 4)} if hbm_bound else
                  {'bound': 'mfma' if mfma else 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
                   'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4)}),
-                traffic=None, kernel='proxy_mfma_kernel' if mfma else 'proxy_kernel',
+                traffic=None, kernel=(('proxy_mfma_stream_kernel (two waves per SIMD, prefetch depth 1)'
+                                       if args.proxy_mode in (0, 3) else
+                                       'proxy_mfma_stream_kernel (one wave per SIMD, prefetch depth 2)'
+                                       if args.proxy_mode == 4 else 'proxy_mfma_kernel (LDS-tiled)'
+                                       if args.proxy_mode == 2 else 'proxy_kernel') if mfma else 'proxy_kernel'),
                 kernel_avg_us=round(kern_s * 1e6, 1), flop_per_row=flop_row, bytes_per_row=bytes_row,
                 fp64_view={'achieved_TFs': round(tflops, 2), 'peak_TFs': FP64_VALU_PEAK_TFS,
                            'frac': round(tflops / FP64_VALU_PEAK_TFS, 4)},

@@ -287,6 +287,129 @@ __global__ __launch_bounds__(kThreads, 2) void proxy_mfma_kernel(ProxyArgs a) {
     }
 }
 
+// ---- 16 < d <= 64, streaming form: every wave on its own 16-row subtiles, no LDS, no barriers ----
+// The transposed product y^T = P dev^T on v_mfma_f64_16x16x4_f64: A = P (16 output columns x 4 k per
+// MFMA, register-resident for the whole kernel), B = dev^T (4 k x 16 sample rows), so lane l holds
+// sample row l & 15 throughout.  The contraction index k and the output columns are permuted (kmap /
+// jmap) such that
+//   * the B fragment of MFMA step s for lane group lk = l >> 4 is k = 8(s >> 1) + 2 lk + (s & 1): the
+//     lane loads its row's k pairs {8t + 2 lk, +1} with ONE 16-byte load each (16 rows x 64 B per
+//     wave instruction), straight from the row-major (n, d) input into registers;
+//   * the output column of D row i = lk + 4r in tile c is 16c + 8(r >> 1) + 2 lk + (r & 1), i.e.
+//     exactly the input column of step s = 4c + r: each lane already holds dev at every column whose
+//     y it holds, so the Mahalanobis term dev . y is a register dot + two cross-lane adds, and the
+//     grad row is written as 16-byte pairs (16 rows x 64 B per instruction).
+// Summation order differs from NumPy's einsum / scipy's BLAS (fp64 tolerance, as the other kernels).
+// Subtiles are prefetched DEPTH ahead in registers; the only traffic is x in, grad + log q out.
+__device__ __forceinline__ int kmap(int s, int lk) { return 8 * (s >> 1) + 2 * lk + (s & 1); }
+__device__ __forceinline__ int jmap(int c, int i) { return 16 * c + 8 * (i >> 3) + 2 * (i & 3) + ((i >> 2) & 1); }
+
+template <int T, int S, bool EVEN, int DEPTH, int BPC>
+__global__ __launch_bounds__(kThreads, BPC) void proxy_mfma_stream_kernel(ProxyArgs a) {
+    static_assert(S % 2 == 0 && S <= 4 * T, "k steps pair up; every step has an output tile");
+    const int d = a.d;
+    const int lane = threadIdx.x & 63;
+    const int li = lane & 15, lk = lane >> 4;
+    double pa[T][S];   // A fragments: P[jmap(c, li)][kmap(s, lk)]
+#pragma unroll
+    for (int c = 0; c < T; ++c) {
+        const int j = jmap(c, li);
+#pragma unroll
+        for (int s = 0; s < S; ++s) {
+            const int k = kmap(s, lk);
+            pa[c][s] = (j < d && k < d) ? a.P[(int64_t)j * d + k] : 0.0;
+        }
+    }
+    __shared__ __attribute__((aligned(16))) double s_loc[8 * (S / 2)];   // loc, zero past d (read in pairs)
+    for (int k = threadIdx.x; k < 8 * (S / 2); k += kThreads) s_loc[k] = k < d ? a.loc[k] : 0.0;
+    __syncthreads();   // the kernel's only barrier
+    const int64_t nsub = (a.n + 15) >> 4;
+    const int64_t wstride = (int64_t)gridDim.x * (kThreads / 64);
+    int64_t sub = (int64_t)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+    auto load = [&](int64_t sb, double (&v)[S]) {
+        int64_t row = sb * 16 + li;
+        row = row < a.n ? row : a.n - 1;   // rows past n: a valid row, results dropped
+        const double* xr = a.x + row * d;
+#pragma unroll
+        for (int t = 0; t < S / 2; ++t) {
+            const int k0 = 8 * t + 2 * lk;
+            if constexpr (EVEN) {   // d even: k0 and k0 + 1 are both < d or both >= d; 16-B aligned
+                typedef double dbl2 __attribute__((ext_vector_type(2)));
+                const dbl2 q = k0 < d ? *reinterpret_cast<const dbl2*>(xr + k0) : dbl2{0.0, 0.0};
+                v[2 * t] = q.x;
+                v[2 * t + 1] = q.y;
+            } else {
+                v[2 * t] = k0 < d ? xr[k0] : 0.0;
+                v[2 * t + 1] = k0 + 1 < d ? xr[k0 + 1] : 0.0;
+            }
+        }
+    };
+    double nx[DEPTH][S];
+#pragma unroll
+    for (int q = 0; q < DEPTH; ++q)
+        if (sub + q * wstride < nsub) load(sub + q * wstride, nx[q]);
+    const double t_df = 0.5 * (a.df + (double)d);
+    for (; sub < nsub; sub += wstride) {
+        double dev[S];
+#pragma unroll
+        for (int t = 0; t < S / 2; ++t) {   // loc pairs from LDS (the 16 lanes of a group read one address)
+            typedef double dbl2 __attribute__((ext_vector_type(2)));
+            const dbl2 lp = *reinterpret_cast<const dbl2*>(s_loc + 8 * t + 2 * lk);
+            dev[2 * t] = nx[0][2 * t] - lp.x;
+            dev[2 * t + 1] = nx[0][2 * t + 1] - lp.y;
+        }
+#pragma unroll
+        for (int q = 0; q + 1 < DEPTH; ++q)
+#pragma unroll
+            for (int s = 0; s < S; ++s) nx[q][s] = nx[q + 1][s];
+        if (sub + DEPTH * wstride < nsub) load(sub + DEPTH * wstride, nx[DEPTH - 1]);
+        dbl4 acc[T];
+#pragma unroll
+        for (int c = 0; c < T; ++c) acc[c] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+        for (int s = 0; s < S; ++s)
+#pragma unroll
+            for (int c = 0; c < T; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[c][s], dev[s], acc[c], 0, 0, 0);
+        // dev . y over this lane's columns (step 4c + r <-> output (c, r)), then over the 4 lanes of the row
+        double part = 0.0;
+#pragma unroll
+        for (int c = 0; c < T; ++c)
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+                if (4 * c + r < S) part = fma(dev[4 * c + r], acc[c][r], part);
+        part += __shfl_xor(part, 16);
+        const double maha = part + __shfl_xor(part, 32);
+        double coef, lq;
+        if (a.df > 0.0) {
+            lq = a.c_log + -t_df * log(1.0 + (1.0 / a.df) * maha);
+            coef = (-(a.df + (double)d) / a.df) / (1.0 + maha / a.df);
+        } else {
+            lq = -0.5 * (a.c_log + maha);
+            coef = -1.0;
+        }
+        const int64_t row = sub * 16 + li;
+        if (row < a.n) {
+            if (lk == 0) a.log_q[row] = lq;
+            double* gr = a.grad + row * d;
+#pragma unroll
+            for (int c = 0; c < T; ++c)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    const int j0 = 16 * c + 8 * h + 2 * lk;
+                    const double g0 = coef == -1.0 ? -acc[c][2 * h] : coef * acc[c][2 * h];
+                    const double g1 = coef == -1.0 ? -acc[c][2 * h + 1] : coef * acc[c][2 * h + 1];
+                    if constexpr (EVEN) {
+                        typedef double dbl2 __attribute__((ext_vector_type(2)));
+                        if (j0 < d) *reinterpret_cast<dbl2*>(gr + j0) = dbl2{g0, g1};
+                    } else {
+                        if (j0 < d) gr[j0] = g0;
+                        if (j0 + 1 < d) gr[j0 + 1] = g1;
+                    }
+                }
+        }
+    }
+}
+
 }  // namespace
 
 int64_t proxy_lds_bytes(int d) { return ((int64_t)2 * d * kPitch + 4 * kRows + d) * 8; }
@@ -296,17 +419,57 @@ static int64_t proxy_mfma_lds_bytes(int d) {
     return ((int64_t)kRows * mfma_pitch(dk) + (int64_t)kRows * (d + 1) + 5 * kRows + d) * 8;
 }
 
-static int g_proxy_mode = 0;   // 0: auto (matrix cores for 16 < d <= 64), 1: always the VALU kernel
+// st_tune key 7: 0 auto (the streaming matrix-core kernel for 16 < d <= 64), 1 always the VALU
+// kernel, 2 the LDS-tiled matrix-core kernel, 3 / 4 streaming with prefetch depth 1 at two waves
+// per SIMD / depth 2 at one wave per SIMD (3 is the auto choice)
+static int g_proxy_mode = 0;
 
 int proxy_tune(int value) {
-    if (value != 0 && value != 1) return -1;
+    if (value < 0 || value > 4) return -1;
     g_proxy_mode = value;
     return 0;
 }
 
+template <int T, int S, bool EVEN, int DEPTH, int BPC>
+static hipError_t launch_stream(const ProxyArgs& a, hipStream_t s) {
+    const int64_t subs = (a.n + 15) / 16;
+    int dev = 0, cus = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    const int64_t waves = (subs + 1) / 2;   // at least two subtiles per wave
+    int64_t grid = (waves + 3) / 4;
+    if (grid > (int64_t)cus * BPC) grid = (int64_t)cus * BPC;
+    if (grid < 1) grid = 1;
+    proxy_mfma_stream_kernel<T, S, EVEN, DEPTH, BPC><<<dim3((unsigned)grid), kThreads, 0, s>>>(a);
+    return hipGetLastError();
+}
+
+template <int T, int S, bool EVEN>
+static hipError_t launch_stream_mode(const ProxyArgs& a, hipStream_t s, int mode) {
+    return mode == 4 ? launch_stream<T, S, EVEN, 2, 1>(a, s) : launch_stream<T, S, EVEN, 1, 2>(a, s);
+}
+
+template <bool EVEN>
+static hipError_t launch_stream_d(const ProxyArgs& a, hipStream_t s, int mode) {
+    const int S = 2 * ((a.d + 7) / 8);
+    switch (S) {
+        case 6: return launch_stream_mode<2, 6, EVEN>(a, s, mode);
+        case 8: return launch_stream_mode<2, 8, EVEN>(a, s, mode);
+        case 10: return launch_stream_mode<3, 10, EVEN>(a, s, mode);
+        case 12: return launch_stream_mode<3, 12, EVEN>(a, s, mode);
+        case 14: return launch_stream_mode<4, 14, EVEN>(a, s, mode);
+        default: return launch_stream_mode<4, 16, EVEN>(a, s, mode);
+    }
+}
+
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
-    if (g_proxy_mode == 0 && a.d > 16 && a.d <= kMfmaMaxD) {
+    if (g_proxy_mode != 1 && g_proxy_mode != 2 && a.d > 16 && a.d <= kMfmaMaxD) {
+        const int mode = g_proxy_mode == 0 ? 3 : g_proxy_mode;
+        return (a.d % 2 == 0) ? launch_stream_d<true>(a, s, mode) : launch_stream_d<false>(a, s, mode);
+    }
+    if (g_proxy_mode == 2 && a.d > 16 && a.d <= kMfmaMaxD) {
         const int64_t lds = proxy_mfma_lds_bytes(a.d);   // <= 69 KB at d = 64
         static bool s_set = false;
         if (!s_set) {

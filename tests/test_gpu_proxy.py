@@ -107,3 +107,25 @@ def test_valu_and_matrix_core_kernels_agree(d):
     for lq, gq in ((lm, gm), (lv_, gv)):
         _close(lq, wl)
         _close(gq, wg)
+
+
+@pytest.mark.parametrize('mode', [2, 3, 4])
+@pytest.mark.parametrize('d', [17, 18, 24, 25, 31, 40, 47, 49, 50, 57, 63, 64])
+def test_matrix_core_variants_match_scipy(mode, d):
+    """Every matrix-core variant (st_tune key 7: 2 LDS-tiled, 3 streaming two waves per SIMD -- the
+    default --, 4 streaming one wave per SIMD with depth-2 prefetch) over each (T, S) instantiation
+    and both the 16-B (even d) and 8-B (odd d) load paths; n not a multiple of 16; both proxies."""
+    from stein_thinning import _native as nat
+    x, mean, cov = _case(1237, d, 7 * d + mode)
+    wl, wg = op.gaussian_proxy(x, mean, cov)
+    tl, tg = op.student_t_proxy(x, mean, cov * 2, 3.5)
+    assert nat.lib().st_tune(7, mode) == 0
+    try:
+        lq, gq = proxy.gaussian_proxy(x, mean, cov)
+        ltq, gtq = proxy.student_t_proxy(x, mean, cov * 2, 3.5)
+    finally:
+        nat.lib().st_tune(7, 0)
+    _close(lq, wl)
+    _close(gq, wg)
+    _close(ltq, tl)
+    _close(gtq, tg)
