@@ -672,11 +672,9 @@ def main_proxy(args):
                   'frac': round(gbs / HBM_PEAK_GBS, 4)} if hbm_bound else
                  {'bound': 'mfma' if mfma else 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
                   'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4)}),
-                traffic=None, kernel=(('proxy_mfma_stream_kernel (two waves per SIMD, prefetch depth 1)'
-                                       if args.proxy_mode in (0, 3) else
-                                       'proxy_mfma_stream_kernel (one wave per SIMD, prefetch depth 2)'
-                                       if args.proxy_mode == 4 else 'proxy_mfma_kernel (LDS-tiled)'
-                                       if args.proxy_mode == 2 else 'proxy_kernel') if mfma else 'proxy_kernel'),
+                traffic=None, kernel=(('proxy_mfma_buf_kernel<4,14>' if args.proxy_mode in (0, 4) and d % 2 == 0
+                                       else 'proxy_mfma_stream_kernel<4,14>' if args.proxy_mode in (0, 3, 4)
+                                       else 'proxy_mfma_kernel (LDS-tiled)') if mfma else 'proxy_kernel'),
                 kernel_avg_us=round(kern_s * 1e6, 1), flop_per_row=flop_row, bytes_per_row=bytes_row,
                 fp64_view={'achieved_TFs': round(tflops, 2), 'peak_TFs': FP64_VALU_PEAK_TFS,
                            'frac': round(tflops / FP64_VALU_PEAK_TFS, 4)},

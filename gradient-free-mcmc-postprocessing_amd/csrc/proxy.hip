@@ -287,7 +287,7 @@ __global__ __launch_bounds__(kThreads, 2) void proxy_mfma_kernel(ProxyArgs a) {
     }
 }
 
-// ---- 16 < d <= 64, streaming form: every wave on its own 16-row subtiles, no LDS, no barriers ----
+// ---- 16 < d <= 64, streaming form: every wave on its own 16-row blocks, no tiles, no barriers ----
 // The transposed product y^T = P dev^T on v_mfma_f64_16x16x4_f64: A = P (16 output columns x 4 k per
 // MFMA, register-resident for the whole kernel), B = dev^T (4 k x 16 sample rows), so lane l holds
 // sample row l & 15 throughout.  The contraction index k and the output columns are permuted (kmap /
@@ -297,30 +297,178 @@ __global__ __launch_bounds__(kThreads, 2) void proxy_mfma_kernel(ProxyArgs a) {
 //     wave instruction), straight from the row-major (n, d) input into registers;
 //   * the output column of D row i = lk + 4r in tile c is 16c + 8(r >> 1) + 2 lk + (r & 1), i.e.
 //     exactly the input column of step s = 4c + r: each lane already holds dev at every column whose
-//     y it holds, so the Mahalanobis term dev . y is a register dot + two cross-lane adds, and the
-//     grad row is written as 16-byte pairs (16 rows x 64 B per instruction).
+//     y it holds, so the Mahalanobis term dev . y is a register dot plus two cross-lane adds.
 // Summation order differs from NumPy's einsum / scipy's BLAS (fp64 tolerance, as the other kernels).
-// Subtiles are prefetched DEPTH ahead in registers; the only traffic is x in, grad + log q out.
+//
+// Two forms (st_tune key 7; profiles/r02_proxy_variants.log has the measured alternatives):
+//   * proxy_mfma_buf_kernel (even d, the default): every global access is a buffer instruction whose
+//     descriptor covers exactly the current 16-row block, so padding columns and rows past n are
+//     out-of-range lanes (loads return 0, stores are dropped) -- no exec-masked branches, a fixed
+//     number of memory instructions per iteration, and the compiler's vmcnt waits count exactly
+//     (the guarded form's loop waits vmcnt(0) every iteration).  The block's grad rows go through a
+//     wave-private LDS slab and out as contiguous 16-B-per-lane stores (whole lines: the fragment
+//     layout's own 64-B row pieces straddle lines and cost 91 vs 81 us of memory time).  The next
+//     block's loads are issued as soon as dev is formed, under this block's MFMAs; two waves per SIMD.
+//   * proxy_mfma_stream_kernel (odd d): 8-B loads/stores guarded per lane, one wave per SIMD with a
+//     two-block prefetch.
+// Diagnostic builds only (tools/proxy_probe.cpp, never the product library): ST_PROXY_DIAG 1 = no
+// MFMAs (memory traffic and epilogue alone), 2 = no grad stores, 3 = neither.
+#ifndef ST_PROXY_DIAG
+#define ST_PROXY_DIAG 0
+#endif
+
 __device__ __forceinline__ int kmap(int s, int lk) { return 8 * (s >> 1) + 2 * lk + (s & 1); }
 __device__ __forceinline__ int jmap(int c, int i) { return 16 * c + 8 * (i >> 3) + 2 * (i & 3) + ((i >> 2) & 1); }
 
-template <int T, int S, bool EVEN, int DEPTH, int BPC>
-__global__ __launch_bounds__(kThreads, BPC) void proxy_mfma_stream_kernel(ProxyArgs a) {
-    static_assert(S % 2 == 0 && S <= 4 * T, "k steps pair up; every step has an output tile");
-    const int d = a.d;
-    const int lane = threadIdx.x & 63;
-    const int li = lane & 15, lk = lane >> 4;
-    double pa[T][S];   // A fragments: P[jmap(c, li)][kmap(s, lk)]
+// A fragments of P for this lane: pa[c][s] = P[jmap(c, l & 15)][kmap(s, l >> 4)] (zero past d)
+template <int T, int S>
+__device__ __forceinline__ void load_p_fragments(const ProxyArgs& a, int li, int lk, double (&pa)[T][S]) {
 #pragma unroll
     for (int c = 0; c < T; ++c) {
         const int j = jmap(c, li);
 #pragma unroll
         for (int s = 0; s < S; ++s) {
             const int k = kmap(s, lk);
-            pa[c][s] = (j < d && k < d) ? a.P[(int64_t)j * d + k] : 0.0;
+            pa[c][s] = (j < a.d && k < a.d) ? a.P[(int64_t)j * a.d + k] : 0.0;
         }
     }
-    __shared__ __attribute__((aligned(16))) double s_loc[8 * (S / 2)];   // loc, zero past d (read in pairs)
+}
+
+// acc[c] = y for this lane's row at output columns jmap(c, lk + 4r), r = 0..3
+template <int T, int S>
+__device__ __forceinline__ void mfma_rows(const double (&pa)[T][S], const double (&dev)[S], dbl4 (&acc)[T]) {
+#pragma unroll
+    for (int c = 0; c < T; ++c) acc[c] = dbl4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int s = 0; s < S; ++s)
+#pragma unroll
+        for (int c = 0; c < T; ++c) {
+            if constexpr (ST_PROXY_DIAG & 1) acc[c][s & 3] += pa[c][s] * dev[s];
+            else acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[c][s], dev[s], acc[c], 0, 0, 0);
+        }
+}
+
+// Mahalanobis term of the lane's row (dev . y, step 4c + r <-> output (c, r), then the 4 lanes of the
+// row), and the row's log q and grad coefficient
+template <int T, int S>
+__device__ __forceinline__ void row_terms(const ProxyArgs& a, const double (&dev)[S], const dbl4 (&acc)[T],
+                                          double& lq, double& coef) {
+    double part = 0.0;
+#pragma unroll
+    for (int c = 0; c < T; ++c)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+            if (4 * c + r < S) part = fma(dev[4 * c + r], acc[c][r], part);
+    part += __shfl_xor(part, 16);
+    const double maha = part + __shfl_xor(part, 32);
+    if (a.df > 0.0) {
+        const double t = 0.5 * (a.df + (double)a.d);
+        lq = a.c_log + -t * log(1.0 + (1.0 / a.df) * maha);
+        coef = (-(a.df + (double)a.d) / a.df) / (1.0 + maha / a.df);
+    } else {
+        lq = -0.5 * (a.c_log + maha);
+        coef = -1.0;
+    }
+}
+
+__device__ __forceinline__ double scaled(double coef, double y) { return coef == -1.0 ? -y : coef * y; }   // Gaussian: exact negation
+
+template <int T, int S>
+__global__ __launch_bounds__(kThreads, 2) void proxy_mfma_buf_kernel(ProxyArgs a) {
+    static_assert(S % 2 == 0 && S <= 4 * T, "k steps pair up; every step has an output tile");
+    typedef double dbl2 __attribute__((ext_vector_type(2)));
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    constexpr int kPairs = S / 2;      // 16-B loads per lane per block; also its 16-B output chunks
+    constexpr uint32_t kOob = 0x80000000u;
+    const int d = a.d;
+    const int lane = threadIdx.x & 63;
+    const int li = lane & 15, lk = lane >> 4;
+    double pa[T][S];
+    load_p_fragments(a, li, lk, pa);
+    __shared__ __attribute__((aligned(16))) double s_loc[8 * kPairs];
+    __shared__ __attribute__((aligned(16))) double s_out[(kThreads / 64) * 16 * 8 * kPairs];
+    double* slab = s_out + (threadIdx.x >> 6) * 16 * d;   // this wave's 16 x d block
+    for (int k = threadIdx.x; k < 8 * kPairs; k += kThreads) s_loc[k] = k < d ? a.loc[k] : 0.0;
+    __syncthreads();   // the kernel's only barrier
+    const int64_t nsub = (a.n + 15) >> 4;
+    const int64_t wstride = (int64_t)gridDim.x * (kThreads / 64);
+    // wave-uniform (SGPR) block index: the descriptors built from it are scalar, no waterfall loops
+    const int64_t sub0 = (int64_t)blockIdx.x * (kThreads / 64) + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    // descriptor over block sb's valid rows (none past the end of the array)
+    auto block_rsrc = [&](const double* base, int64_t sb, int per_row) {
+        const int64_t r0 = sb * 16;
+        const int64_t rows = r0 < a.n ? min<int64_t>(16, a.n - r0) : 0;
+        const double* p = base + (r0 < a.n ? r0 : 0) * per_row;
+        return __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(p), 0, (int)(rows * per_row * 8), 0x00020000);
+    };
+    auto load = [&](int64_t sb, dbl2 (&v)[kPairs]) {   // row li, column pairs k0 = 8t + 2 lk
+        const auto rs = block_rsrc(a.x, sb, d);
+#pragma unroll
+        for (int t = 0; t < kPairs; ++t) {
+            const int k0 = 8 * t + 2 * lk;
+            const u32x4 q = __builtin_amdgcn_raw_buffer_load_b128(rs, k0 < d ? (uint32_t)((li * d + k0) * 8) : kOob, 0, 0);
+            v[t] = dbl2{__builtin_bit_cast(double, u32x2{q.x, q.y}), __builtin_bit_cast(double, u32x2{q.z, q.w})};
+        }
+    };
+    dbl2 buf[kPairs];
+    load(sub0, buf);
+    for (int64_t sb = sub0; sb < nsub; sb += wstride) {
+        double dev[S];
+#pragma unroll
+        for (int t = 0; t < kPairs; ++t) {
+            const dbl2 lp = *reinterpret_cast<const dbl2*>(s_loc + 8 * t + 2 * lk);
+            dev[2 * t] = buf[t].x - lp.x;
+            dev[2 * t + 1] = buf[t].y - lp.y;
+        }
+        load(sb + wstride, buf);   // past the end: an empty descriptor, no traffic
+        dbl4 acc[T];
+        mfma_rows(pa, dev, acc);
+        double lq, coef;
+        row_terms(a, dev, acc, lq, coef);
+        {   // log q from the lk == 0 lanes; rows past n are out of range
+            const auto rs = block_rsrc(a.log_q, sb, 1);
+            const uint64_t lb = (uint64_t)__double_as_longlong(lq);
+            __builtin_amdgcn_raw_buffer_store_b64(u32x2{(unsigned)lb, (unsigned)(lb >> 32)}, rs,
+                                                  lk == 0 ? (uint32_t)(li * 8) : kOob, 0, 0);
+        }
+        if constexpr (ST_PROXY_DIAG & 2) continue;
+        // grad rows into the slab at their global layout (row li at slab[li d]) ...
+#pragma unroll
+        for (int c = 0; c < T; ++c)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int j0 = 16 * c + 8 * h + 2 * lk;
+                if (j0 < d)
+                    *reinterpret_cast<dbl2*>(slab + li * d + j0) =
+                        dbl2{scaled(coef, acc[c][2 * h]), scaled(coef, acc[c][2 * h + 1])};
+            }
+        __builtin_amdgcn_wave_barrier();
+        // ... and out as contiguous 16-B-per-lane stores of the whole 16 d-double block
+        const auto rs = block_rsrc(a.grad, sb, d);
+#pragma unroll
+        for (int i = 0; i < kPairs; ++i) {
+            const int e = 2 * (lane + 64 * i);
+            const bool in = e < 16 * d;
+            const dbl2 v = *reinterpret_cast<const dbl2*>(slab + (in ? e : 0));
+            const uint64_t v0 = (uint64_t)__double_as_longlong(v.x), v1 = (uint64_t)__double_as_longlong(v.y);
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)v0, (unsigned)(v0 >> 32), (unsigned)v1, (unsigned)(v1 >> 32)},
+                                                   rs, in ? (uint32_t)(e * 8) : kOob, 0, 0);
+        }
+        __builtin_amdgcn_wave_barrier();   // the slab's reads are issued before the next block's writes
+    }
+}
+
+template <int T, int S>
+__global__ __launch_bounds__(kThreads, 1) void proxy_mfma_stream_kernel(ProxyArgs a) {
+    static_assert(S % 2 == 0 && S <= 4 * T, "k steps pair up; every step has an output tile");
+    constexpr int kDepth = 2;   // blocks in flight per wave
+    const int d = a.d;
+    const int lane = threadIdx.x & 63;
+    const int li = lane & 15, lk = lane >> 4;
+    double pa[T][S];
+    load_p_fragments(a, li, lk, pa);
+    __shared__ __attribute__((aligned(16))) double s_loc[8 * (S / 2)];
     for (int k = threadIdx.x; k < 8 * (S / 2); k += kThreads) s_loc[k] = k < d ? a.loc[k] : 0.0;
     __syncthreads();   // the kernel's only barrier
     const int64_t nsub = (a.n + 15) >> 4;
@@ -333,78 +481,39 @@ __global__ __launch_bounds__(kThreads, BPC) void proxy_mfma_stream_kernel(ProxyA
 #pragma unroll
         for (int t = 0; t < S / 2; ++t) {
             const int k0 = 8 * t + 2 * lk;
-            if constexpr (EVEN) {   // d even: k0 and k0 + 1 are both < d or both >= d; 16-B aligned
-                typedef double dbl2 __attribute__((ext_vector_type(2)));
-                const dbl2 q = k0 < d ? *reinterpret_cast<const dbl2*>(xr + k0) : dbl2{0.0, 0.0};
-                v[2 * t] = q.x;
-                v[2 * t + 1] = q.y;
-            } else {
-                v[2 * t] = k0 < d ? xr[k0] : 0.0;
-                v[2 * t + 1] = k0 + 1 < d ? xr[k0 + 1] : 0.0;
-            }
+            v[2 * t] = k0 < d ? xr[k0] : 0.0;
+            v[2 * t + 1] = k0 + 1 < d ? xr[k0 + 1] : 0.0;
         }
     };
-    double nx[DEPTH][S];
+    double nx[kDepth][S];
 #pragma unroll
-    for (int q = 0; q < DEPTH; ++q)
+    for (int q = 0; q < kDepth; ++q)
         if (sub + q * wstride < nsub) load(sub + q * wstride, nx[q]);
-    const double t_df = 0.5 * (a.df + (double)d);
     for (; sub < nsub; sub += wstride) {
         double dev[S];
 #pragma unroll
-        for (int t = 0; t < S / 2; ++t) {   // loc pairs from LDS (the 16 lanes of a group read one address)
-            typedef double dbl2 __attribute__((ext_vector_type(2)));
-            const dbl2 lp = *reinterpret_cast<const dbl2*>(s_loc + 8 * t + 2 * lk);
-            dev[2 * t] = nx[0][2 * t] - lp.x;
-            dev[2 * t + 1] = nx[0][2 * t + 1] - lp.y;
-        }
+        for (int s = 0; s < S; ++s) dev[s] = nx[0][s] - s_loc[kmap(s, lk)];
 #pragma unroll
-        for (int q = 0; q + 1 < DEPTH; ++q)
+        for (int q = 0; q + 1 < kDepth; ++q)
 #pragma unroll
             for (int s = 0; s < S; ++s) nx[q][s] = nx[q + 1][s];
-        if (sub + DEPTH * wstride < nsub) load(sub + DEPTH * wstride, nx[DEPTH - 1]);
+        if (sub + kDepth * wstride < nsub) load(sub + kDepth * wstride, nx[kDepth - 1]);
         dbl4 acc[T];
-#pragma unroll
-        for (int c = 0; c < T; ++c) acc[c] = dbl4{0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int s = 0; s < S; ++s)
-#pragma unroll
-            for (int c = 0; c < T; ++c) acc[c] = __builtin_amdgcn_mfma_f64_16x16x4f64(pa[c][s], dev[s], acc[c], 0, 0, 0);
-        // dev . y over this lane's columns (step 4c + r <-> output (c, r)), then over the 4 lanes of the row
-        double part = 0.0;
-#pragma unroll
-        for (int c = 0; c < T; ++c)
-#pragma unroll
-            for (int r = 0; r < 4; ++r)
-                if (4 * c + r < S) part = fma(dev[4 * c + r], acc[c][r], part);
-        part += __shfl_xor(part, 16);
-        const double maha = part + __shfl_xor(part, 32);
-        double coef, lq;
-        if (a.df > 0.0) {
-            lq = a.c_log + -t_df * log(1.0 + (1.0 / a.df) * maha);
-            coef = (-(a.df + (double)d) / a.df) / (1.0 + maha / a.df);
-        } else {
-            lq = -0.5 * (a.c_log + maha);
-            coef = -1.0;
-        }
+        mfma_rows(pa, dev, acc);
+        double lq, coef;
+        row_terms(a, dev, acc, lq, coef);
         const int64_t row = sub * 16 + li;
         if (row < a.n) {
             if (lk == 0) a.log_q[row] = lq;
+            if constexpr (ST_PROXY_DIAG & 2) continue;
             double* gr = a.grad + row * d;
 #pragma unroll
             for (int c = 0; c < T; ++c)
 #pragma unroll
                 for (int h = 0; h < 2; ++h) {
                     const int j0 = 16 * c + 8 * h + 2 * lk;
-                    const double g0 = coef == -1.0 ? -acc[c][2 * h] : coef * acc[c][2 * h];
-                    const double g1 = coef == -1.0 ? -acc[c][2 * h + 1] : coef * acc[c][2 * h + 1];
-                    if constexpr (EVEN) {
-                        typedef double dbl2 __attribute__((ext_vector_type(2)));
-                        if (j0 < d) *reinterpret_cast<dbl2*>(gr + j0) = dbl2{g0, g1};
-                    } else {
-                        if (j0 < d) gr[j0] = g0;
-                        if (j0 + 1 < d) gr[j0 + 1] = g1;
-                    }
+                    if (j0 < d) gr[j0] = scaled(coef, acc[c][2 * h]);
+                    if (j0 + 1 < d) gr[j0 + 1] = scaled(coef, acc[c][2 * h + 1]);
                 }
         }
     }
@@ -419,9 +528,9 @@ static int64_t proxy_mfma_lds_bytes(int d) {
     return ((int64_t)kRows * mfma_pitch(dk) + (int64_t)kRows * (d + 1) + 5 * kRows + d) * 8;
 }
 
-// st_tune key 7: 0 auto (the streaming matrix-core kernel for 16 < d <= 64), 1 always the VALU
-// kernel, 2 the LDS-tiled matrix-core kernel, 3 / 4 streaming with prefetch depth 1 at two waves
-// per SIMD / depth 2 at one wave per SIMD (3 is the auto choice)
+// st_tune key 7: 0 auto (16 < d <= 64: the buffer form for even d, the guarded streaming form for
+// odd d), 1 always the VALU kernel, 2 the LDS-tiled matrix-core kernel (round 1), 3 the guarded
+// streaming form for any d, 4 the buffer form (even d; odd d runs 3)
 static int g_proxy_mode = 0;
 
 int proxy_tune(int value) {
@@ -430,45 +539,44 @@ int proxy_tune(int value) {
     return 0;
 }
 
-template <int T, int S, bool EVEN, int DEPTH, int BPC>
-static hipError_t launch_stream(const ProxyArgs& a, hipStream_t s) {
-    const int64_t subs = (a.n + 15) / 16;
+static hipError_t grid_for(const ProxyArgs& a, int bpc, int64_t& grid) {
     int dev = 0, cus = 0;
     hipError_t e = hipGetDevice(&dev);
     if (e != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-    const int64_t waves = (subs + 1) / 2;   // at least two subtiles per wave
-    int64_t grid = (waves + 3) / 4;
-    if (grid > (int64_t)cus * BPC) grid = (int64_t)cus * BPC;
+    const int64_t waves = ((a.n + 15) / 16 + 1) / 2;   // at least two blocks per wave
+    grid = (waves + kThreads / 64 - 1) / (kThreads / 64);
+    if (grid > (int64_t)cus * bpc) grid = (int64_t)cus * bpc;
     if (grid < 1) grid = 1;
-    proxy_mfma_stream_kernel<T, S, EVEN, DEPTH, BPC><<<dim3((unsigned)grid), kThreads, 0, s>>>(a);
+    return hipSuccess;
+}
+
+template <int T, int S>
+static hipError_t launch_stream_ts(const ProxyArgs& a, hipStream_t s, bool buffered) {
+    int64_t grid = 0;
+    hipError_t e = grid_for(a, buffered ? 2 : 1, grid);
+    if (e != hipSuccess) return e;
+    if (buffered) proxy_mfma_buf_kernel<T, S><<<dim3((unsigned)grid), kThreads, 0, s>>>(a);
+    else proxy_mfma_stream_kernel<T, S><<<dim3((unsigned)grid), kThreads, 0, s>>>(a);
     return hipGetLastError();
 }
 
-template <int T, int S, bool EVEN>
-static hipError_t launch_stream_mode(const ProxyArgs& a, hipStream_t s, int mode) {
-    return mode == 4 ? launch_stream<T, S, EVEN, 2, 1>(a, s) : launch_stream<T, S, EVEN, 1, 2>(a, s);
-}
-
-template <bool EVEN>
-static hipError_t launch_stream_d(const ProxyArgs& a, hipStream_t s, int mode) {
-    const int S = 2 * ((a.d + 7) / 8);
-    switch (S) {
-        case 6: return launch_stream_mode<2, 6, EVEN>(a, s, mode);
-        case 8: return launch_stream_mode<2, 8, EVEN>(a, s, mode);
-        case 10: return launch_stream_mode<3, 10, EVEN>(a, s, mode);
-        case 12: return launch_stream_mode<3, 12, EVEN>(a, s, mode);
-        case 14: return launch_stream_mode<4, 14, EVEN>(a, s, mode);
-        default: return launch_stream_mode<4, 16, EVEN>(a, s, mode);
+// T = ceil(d / 16) output tiles, S = 2 ceil(d / 8) k steps
+static hipError_t launch_stream(const ProxyArgs& a, hipStream_t s, bool buffered) {
+    switch ((a.d + 7) / 8) {
+        case 3: return launch_stream_ts<2, 6>(a, s, buffered);
+        case 4: return launch_stream_ts<2, 8>(a, s, buffered);
+        case 5: return launch_stream_ts<3, 10>(a, s, buffered);
+        case 6: return launch_stream_ts<3, 12>(a, s, buffered);
+        case 7: return launch_stream_ts<4, 14>(a, s, buffered);
+        default: return launch_stream_ts<4, 16>(a, s, buffered);
     }
 }
 
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
-    if (g_proxy_mode != 1 && g_proxy_mode != 2 && a.d > 16 && a.d <= kMfmaMaxD) {
-        const int mode = g_proxy_mode == 0 ? 3 : g_proxy_mode;
-        return (a.d % 2 == 0) ? launch_stream_d<true>(a, s, mode) : launch_stream_d<false>(a, s, mode);
-    }
+    if (g_proxy_mode != 1 && g_proxy_mode != 2 && a.d > 16 && a.d <= kMfmaMaxD)
+        return launch_stream(a, s, a.d % 2 == 0 && g_proxy_mode != 3);
     if (g_proxy_mode == 2 && a.d > 16 && a.d <= kMfmaMaxD) {
         const int64_t lds = proxy_mfma_lds_bytes(a.d);   // <= 69 KB at d = 64
         static bool s_set = false;

@@ -112,9 +112,9 @@ def test_valu_and_matrix_core_kernels_agree(d):
 @pytest.mark.parametrize('mode', [2, 3, 4])
 @pytest.mark.parametrize('d', [17, 18, 24, 25, 31, 40, 47, 49, 50, 57, 63, 64])
 def test_matrix_core_variants_match_scipy(mode, d):
-    """Every matrix-core variant (st_tune key 7: 2 LDS-tiled, 3 streaming two waves per SIMD -- the
-    default --, 4 streaming one wave per SIMD with depth-2 prefetch) over each (T, S) instantiation
-    and both the 16-B (even d) and 8-B (odd d) load paths; n not a multiple of 16; both proxies."""
+    """Every matrix-core variant (st_tune key 7: 2 LDS-tiled, 3 guarded streaming form -- the odd-d
+    default --, 4 buffer-instruction form -- the even-d default; odd d falls back to 3) over each
+    (T, S) instantiation; n not a multiple of 16; both proxies."""
     from stein_thinning import _native as nat
     x, mean, cov = _case(1237, d, 7 * d + mode)
     wl, wg = op.gaussian_proxy(x, mean, cov)
