@@ -277,7 +277,7 @@ def main():
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
     ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
-    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'ranks'],
+    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
                          '(row-sharded, RCCL all-reduce of the n-length column-sum vector); ranks: launcher '
                          'check only (gloo, no GPU)')
@@ -292,6 +292,8 @@ def main():
         return 2
     if args.workload == 'ranks':
         return main_ranks(args)
+    if args.workload == 'energy':
+        return main_energy(args)
     if args.workload == 'ksd':
         return main_ksd(args)
     if args.workload == 'proxy':
@@ -482,6 +484,95 @@ def main():
         }
         print(json.dumps(line), flush=True)
     if sharded:
+        dist.destroy_process_group()
+
+
+def thinned_sizes(n_points_calculate: int = 1000) -> np.ndarray:
+    """Comparison.ipynb cell 21: 50 sizes on [5, 100] and 200 on [100, n_points_calculate]."""
+    return np.concatenate([np.linspace(5, 100, 50).astype(int),
+                           np.linspace(100, n_points_calculate, 200).astype(int)])
+
+
+def main_energy(args):
+    """The reference's fit_quality curve (Comparison.ipynb cells 19-23): sqrt(dcor.energy_distance(
+    validation[::10], sample[idx[:k]])) for the 250 thinned sizes k of cell 21, on the config-4 scale:
+    validation = a second seeded LV-surrogate pool of 2e6 points (the reference's validation HMC chains
+    live in S3) taken [::10] -> 2e5 points; sample / idx = config 4's sample and its m = 1000 Stein
+    thinning.  A step = one whole curve, inputs resident on the GPU (stein_thinning.energy.EnergyCurve:
+    the validation set's triangle once, the cross block, the selection's triangle).  N > 1: replicas
+    (each rank evaluates the whole curve; the reference evaluates one curve per chain and method)."""
+    import torch
+    import torch.distributed as dist
+    from stein_thinning import energy as se
+    from stein_thinning import thinning as st
+    rank, world, dev = _setup_ranks()
+    if world > 1:
+        _init_group(dev)
+    cfg = CONFIGS['c4']
+    x, g, _, _ = lv_surrogate(cfg['n'], cfg['seed'])
+    validation = lv_surrogate(cfg['n'], cfg['seed'] + 100)[0][::10]
+    idx = st.thin(x, g, cfg['m'], preconditioner='med')
+    sizes = thinned_sizes(cfg['m'])
+    curve = se.EnergyCurve(validation, x[idx])
+    pairs = curve.pair_count()
+    for _ in range(args.warmup):
+        curve.launch(sizes)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        out = curve.launch(sizes)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    step_s = float(np.median([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
+    got = out.cpu().numpy()
+    if world > 1:
+        dist.barrier()
+        elapsed, step_s = _max_over_ranks([elapsed, step_s], dev)
+    if rank == 0:
+        d = x.shape[1]
+        flop_pair = 3 * d + 1   # d sub, d mul, d - 1 add, 1 sqrt, 1 accumulate
+        tflops = pairs * flop_pair / step_s / 1e12
+        line = {
+            'metric': 'energy-distance curve: pair-distance evals/s (fit_quality over 250 prefixes)',
+            'value': pairs * args.steps * world / elapsed, 'unit': 'pair-distance evals/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': elapsed / args.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64',
+            'data': 'synthetic (seeded RW-MH LV-surrogate pools; validation = a second pool [::10])',
+            'config': {'workload': 'fit_quality curve: validation 2e5 x 4 against prefixes of config 4\'s m = 1000 '
+                                   'Stein selection, 250 sizes (Comparison.ipynb cells 19-23)',
+                       'n_validation': int(validation.shape[0]), 'm': int(cfg['m']), 'sizes': int(sizes.size),
+                       'pairs_per_step': int(pairs), 'ed_at_1000': float(got[-1]),
+                       'parallelism': f'replicas x{world}' if world > 1 else 'single-gpu'},
+            'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
+                         'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': None,
+                         'kernel': f'dist_colsum_kernel<{d}> (+ reduce / cumsum)', 'step_median_us': round(step_s * 1e6, 1),
+                         'flop_per_pair': flop_pair,
+                         'note': 'per pair: d differences, squares and sums, one IEEE sqrt (a ~10-instruction '
+                                 'sequence on gfx950) and the accumulate; O(n d) bytes -- fp64 VALU-bound'},
+        }
+        if not args.no_cpu_baseline:
+            from oracle import stein_numpy as ref
+            xs = validation[:10_000]
+            ys = x[idx]
+            c0 = time.perf_counter()
+            ref.energy_distance(xs, ys)
+            dt = time.perf_counter() - c0
+            cpu_pairs = xs.shape[0] ** 2 + xs.shape[0] * ys.shape[0] + ys.shape[0] ** 2
+            ref_pairs = sizes.size * validation.shape[0] ** 2 + int(np.sum(validation.shape[0] * sizes + sizes ** 2))
+            line['cpu_baseline'] = {
+                'value': cpu_pairs / dt, 'unit': 'pair-distance evals/s', 'cores': 1, 'kind': 'port',
+                'sample': (f'oracle.stein_numpy.energy_distance (the reference\'s dcor.energy_distance restated as '
+                           f'scipy cdist means) for validation[:10000] vs the 1000 selected points: {cpu_pairs:.3g} '
+                           f'distances in {dt:.2f} s; the reference\'s curve (one full energy distance per size, '
+                           f'{ref_pairs:.3g} distances) extrapolates to {ref_pairs * dt / cpu_pairs:.0f} s')}
+        print(json.dumps(line), flush=True)
+    if world > 1:
         dist.destroy_process_group()
 
 

@@ -501,9 +501,23 @@ int st_ksd_finish(const double* x_soa, const double* g_soa, const double* weight
                      "ksd finish launch");
 }
 
+int64_t st_distance_workspace_bytes(int64_t na, int64_t b_begin, int64_t b_end) {
+    if (na < 0 || b_begin < 0 || b_end < b_begin) return -1;
+    const int64_t K = st::distance_chunks(na, b_begin, b_end);
+    return K > 1 ? K * na * (int64_t)sizeof(double) : 0;
+}
+
 int st_distance_colsum(const double* a_soa, int64_t lda, int64_t na, const double* b_soa,
                        int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
                        int32_t triangle, double* out, void* stream) {
+    return st_distance_colsum_ws(a_soa, lda, na, b_soa, ldb, nb, d, b_begin, b_end, triangle, out,
+                                 nullptr, 0, stream);
+}
+
+int st_distance_colsum_ws(const double* a_soa, int64_t lda, int64_t na, const double* b_soa,
+                          int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
+                          int32_t triangle, double* out, void* workspace, int64_t workspace_bytes,
+                          void* stream) {
     if (na == 0) return ST_OK;
     if (!a_soa || !b_soa || !out) return fail(ST_ERR_INVALID, "NULL pointer");
     if (d < 1 || d > st::kMaxDim) return fail(ST_ERR_UNSUPPORTED, "unsupported d = %d", d);
@@ -514,8 +528,10 @@ int st_distance_colsum(const double* a_soa, int64_t lda, int64_t na, const doubl
     if (triangle && (a_soa != b_soa || lda != ldb))
         return fail(ST_ERR_INVALID, "triangle=1 needs A and B to be the same array");
     if ((na + 255) / 256 > 0x7FFFFFFFll) return fail(ST_ERR_UNSUPPORTED, "na too large");
+    if (workspace && !aligned16(workspace)) return fail(ST_ERR_INVALID, "workspace must be 16-byte aligned");
     return hip_check(st::launch_distance_colsum(a_soa, lda, na, b_soa, ldb, b_begin, b_end, d,
-                                                triangle ? 1 : 0, out,
+                                                triangle ? 1 : 0, out, static_cast<double*>(workspace),
+                                                workspace ? workspace_bytes / 8 : 0,
                                                 static_cast<hipStream_t>(stream)),
                      "distance column-sum launch");
 }

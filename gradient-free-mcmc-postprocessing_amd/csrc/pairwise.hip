@@ -264,8 +264,16 @@ struct DistArgs {
     int64_t ldb;
     int64_t b0, b1;
     int tri;
-    double* out;
+    double* out;       // K == 1: the sums; K > 1: partial sums [K][na] (reduced by dist_reduce_kernel)
+    int64_t chunk;     // B points per blockIdx.y chunk (multiple of the staging tile)
 };
+
+// B range of this block: chunk blockIdx.y of [b0, b1), cut at the block's last column for the triangle
+__device__ __forceinline__ void dist_range(const DistArgs& p, int64_t c0, int64_t cols, int64_t& lo, int64_t& hi) {
+    lo = p.b0 + (int64_t)blockIdx.y * p.chunk;
+    hi = lo + p.chunk < p.b1 ? lo + p.chunk : p.b1;
+    if (p.tri && c0 + cols < hi) hi = c0 + cols;
+}
 
 template <int D>
 __global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
@@ -279,10 +287,10 @@ __global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
     double ai[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) ai[k] = live ? p.a[k * p.lda + i] : 0.0;
-    int64_t b_stop = p.b1;
-    if (p.tri && c0 + R < b_stop) b_stop = c0 + R;
+    int64_t lo, b_stop;
+    dist_range(p, c0, R, lo, b_stop);
     double acc = 0.0;
-    for (int64_t bc = p.b0; bc < b_stop; bc += R) {
+    for (int64_t bc = lo; bc < b_stop; bc += R) {
         __syncthreads();
         const int64_t bb = bc + tid;
         if (bb < b_stop) {
@@ -302,7 +310,7 @@ __global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
             acc = (!p.tri || bc + e < i) ? acc + dist : acc;
         }
     }
-    if (live) p.out[i] = acc;
+    if (live) p.out[(int64_t)blockIdx.y * p.na + i] = acc;
 }
 
 __global__ __launch_bounds__(kColBlock) void dist_colsum_rt_kernel(DistArgs p, int d) {
@@ -314,10 +322,10 @@ __global__ __launch_bounds__(kColBlock) void dist_colsum_rt_kernel(DistArgs p, i
     const int64_t i = c0 + tid;
     const bool live = i < p.na;
     const int64_t ic = live ? i : 0;
-    int64_t b_stop = p.b1;
-    if (p.tri && c0 + kColBlock < b_stop) b_stop = c0 + kColBlock;
+    int64_t lo, b_stop;
+    dist_range(p, c0, kColBlock, lo, b_stop);
     double acc = 0.0;
-    for (int64_t bc = p.b0; bc < b_stop; bc += R) {
+    for (int64_t bc = lo; bc < b_stop; bc += R) {
         const int cnt = (int)((b_stop - bc) < R ? (b_stop - bc) : R);
         __syncthreads();
         for (int e = tid; e < d * R; e += kColBlock) {
@@ -335,14 +343,41 @@ __global__ __launch_bounds__(kColBlock) void dist_colsum_rt_kernel(DistArgs p, i
             acc = (!p.tri || bc + e < i) ? acc + dist : acc;
         }
     }
-    if (live) p.out[i] = acc;
+    if (live) p.out[(int64_t)blockIdx.y * p.na + i] = acc;
+}
+
+// out[i] = sum over the K chunk partials, in chunk order (deterministic)
+__global__ void dist_reduce_kernel(const double* part, int64_t na, int K, double* out) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= na) return;
+    double acc = part[i];
+    for (int k = 1; k < K; ++k) acc += part[(int64_t)k * na + i];
+    out[i] = acc;
+}
+
+// B chunks per launch: enough blocks to fill the chip (>= 2048 over both grid dimensions) without
+// chunks shorter than four staging tiles (1024 points)
+int64_t distance_chunks(int64_t na, int64_t b_begin, int64_t b_end) {
+    const int64_t ablocks = (na + kColBlock - 1) / kColBlock;
+    const int64_t range = b_end - b_begin;
+    if (ablocks <= 0 || range <= 0) return 1;
+    int64_t K = (2048 + ablocks - 1) / ablocks;
+    const int64_t kmax = (range + 4 * kColBlock - 1) / (4 * kColBlock);
+    if (K > kmax) K = kmax;
+    if (K > 65535) K = 65535;
+    return K < 1 ? 1 : K;
 }
 
 hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, const double* b,
                                   int64_t ldb, int64_t b0, int64_t b1, int d, int tri,
-                                  double* out, hipStream_t s) {
-    DistArgs p{a, lda, na, b, ldb, b0, b1, tri, out};
-    const unsigned grid = (unsigned)((na + kColBlock - 1) / kColBlock);
+                                  double* out, double* ws, int64_t ws_doubles, hipStream_t s) {
+    int64_t K = distance_chunks(na, b0, b1);
+    if (!ws || ws_doubles < K * na) K = 1;   // no workspace: one chunk, sums straight into out
+    const int64_t range = b1 - b0;
+    int64_t chunk = K > 1 ? (range + K - 1) / K : (range > 0 ? range : 1);
+    if (K > 1) chunk = (chunk + kColBlock - 1) / kColBlock * kColBlock;   // whole staging tiles
+    DistArgs p{a, lda, na, b, ldb, b0, b1, tri, K > 1 ? ws : out, chunk};
+    const dim3 grid((unsigned)((na + kColBlock - 1) / kColBlock), (unsigned)K);
     switch (d) {
         case 1: dist_colsum_kernel<1><<<grid, kColBlock, 0, s>>>(p); break;
         case 2: dist_colsum_kernel<2><<<grid, kColBlock, 0, s>>>(p); break;
@@ -354,6 +389,7 @@ hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, cons
         case 8: dist_colsum_kernel<8><<<grid, kColBlock, 0, s>>>(p); break;
         default: dist_colsum_rt_kernel<<<grid, kColBlock, 0, s>>>(p, d); break;
     }
+    if (K > 1) dist_reduce_kernel<<<(unsigned)((na + 255) / 256), 256, 0, s>>>(ws, na, (int)K, out);
     return hipGetLastError();
 }
 

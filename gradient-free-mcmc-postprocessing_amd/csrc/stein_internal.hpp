@@ -133,9 +133,10 @@ hipError_t launch_ksd_colsum(const PairArgs& p, int64_t n, int64_t a0, int64_t a
                              hipStream_t s);
 hipError_t launch_ksd_finish(const PairArgs& p, int64_t n, const double* csum, double* ks,
                              hipStream_t s);
+int64_t distance_chunks(int64_t na, int64_t b_begin, int64_t b_end);
 hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, const double* b,
                                   int64_t ldb, int64_t b0, int64_t b1, int d, int tri,
-                                  double* out, hipStream_t s);
+                                  double* out, double* ws, int64_t ws_doubles, hipStream_t s);
 hipError_t launch_layout_soa(const double* rowmajor, int64_t n, int d, int64_t ld, double* soa,
                              hipStream_t s);
 

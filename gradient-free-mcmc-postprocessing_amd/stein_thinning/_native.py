@@ -57,6 +57,9 @@ SIGNATURES = {
                                      _c_dp, _c_dp]),
     'st_distance_colsum': (ctypes.c_int, [_c_dp, _i64, _i64, _c_dp, _i64, _i64, _i32, _i64, _i64,
                                           _i32, _c_dp, _c_dp]),
+    'st_distance_workspace_bytes': (_i64, [_i64, _i64, _i64]),
+    'st_distance_colsum_ws': (ctypes.c_int, [_c_dp, _i64, _i64, _c_dp, _i64, _i64, _i32, _i64, _i64,
+                                             _i32, _c_dp, _c_dp, _i64, _c_dp]),
     'st_standardize_host': (ctypes.c_int, [_c_dp, _c_dp, _i64, _i32, _i32, _c_dp, _c_dp, _c_dp, _c_dp,
                                            ctypes.POINTER(ctypes.c_int32)]),
     'st_mailbox_bytes': (_i64, [_i32]),

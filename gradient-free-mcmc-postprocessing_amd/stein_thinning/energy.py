@@ -9,8 +9,9 @@ and ``Gaussian_mixture.ipynb`` cells 63-71 evaluate it for prefixes of the selec
 
     ED(x, y) = 2 E|X - Y| - E|X - X'| - E|Y - Y'|      (all means over all ordered pairs)
 
-Device work: K7 (``st_distance_colsum``): per point of A, the sum of Euclidean distances to a range
-of B (or to the earlier points of A itself).  ``energy_distance_curve`` evaluates all prefixes of
+Device work: K7 (``st_distance_colsum_ws``): per point of A, the sum of Euclidean distances to a
+range of B (or to the earlier points of A itself), the B range split over blockIdx.y chunks so that
+a short A (the selected points) against a long B (the validation sample) still fills the chip.  ``energy_distance_curve`` evaluates all prefixes of
 one selection in one pass: the validation set's self term once, the cross sums once per selected
 point, the selection's self sums once -- instead of one dcor call (and one n_v^2 self term) per
 prefix.  Sums of the per-point totals are formed on the host in float64.
@@ -36,13 +37,18 @@ def _soa(points: np.ndarray, device):
     return soa, n, d, ld
 
 
-def _colsum(a, na, lda, b, nb, ldb, d, b0, b1, tri, device):
+def _colsum(a, na, lda, b, nb, ldb, d, b0, b1, tri, device, host=True):
+    """Per point of A: sum of distances to B[b0:b1] (strictly earlier points when tri), with the B
+    range split over enough blocks to fill the GPU (st_distance_colsum_ws)."""
     import torch
+    L = nat.lib()
     out = torch.zeros(max(na, 1), dtype=torch.float64, device=device)
-    nat.check(nat.lib().st_distance_colsum(nat.ptr(a), lda, na, nat.ptr(b), ldb, nb, d, b0, b1,
-                                           1 if tri else 0, nat.ptr(out), nat.stream_handle()),
-              'st_distance_colsum')
-    return out[:na].cpu().numpy()
+    wsb = int(L.st_distance_workspace_bytes(na, b0, b1))
+    ws = torch.empty(max(wsb // 8, 2), dtype=torch.float64, device=device)
+    nat.check(L.st_distance_colsum_ws(nat.ptr(a), lda, na, nat.ptr(b), ldb, nb, d, b0, b1, 1 if tri else 0,
+                                      nat.ptr(out), nat.ptr(ws), ws.numel() * 8, nat.stream_handle()),
+              'st_distance_colsum_ws')
+    return out[:na].cpu().numpy() if host else out[:na]
 
 
 def _points(a) -> np.ndarray:
@@ -71,24 +77,50 @@ def energy_distance(x, y) -> float:
     return float(2.0 * cross / (nx * ny) - 2.0 * xx / (nx * nx) - 2.0 * yy / (ny * ny))
 
 
+class EnergyCurve:
+    """The reference's fit_quality curve, sqrt(ED(reference_points, sample[idx[:k]])) for every k in
+    ``sizes`` (Comparison.ipynb cells 19-23), with both point sets resident on the GPU: the
+    reference set's self term once, the cross sums once per selected point, the selection's self
+    sums once (instead of one full dcor evaluation per prefix)."""
+
+    def __init__(self, reference_points, selection):
+        x, y = _points(reference_points), _points(selection)
+        _check(x, y)
+        self.device = nat.require_device()
+        self.xs, self.nx, self.d, self.ldx = _soa(x, self.device)
+        self.ys, self.ny, _, self.ldy = _soa(y, self.device)
+
+    def pair_count(self) -> int:
+        """Distance evaluations per run: the reference set's triangle, the cross block, the
+        selection's triangle."""
+        return self.nx * (self.nx - 1) // 2 + self.nx * self.ny + self.ny * (self.ny - 1) // 2
+
+    def launch(self, sizes):
+        """Enqueue one curve evaluation (device tensors; no host sync)."""
+        import torch
+        dev, d = self.device, self.d
+        xx = _colsum(self.xs, self.nx, self.ldx, self.xs, self.nx, self.ldx, d, 0, self.nx, True, dev, host=False).sum()
+        cross = torch.cumsum(_colsum(self.ys, self.ny, self.ldy, self.xs, self.nx, self.ldx, d, 0, self.nx, False,
+                                     dev, host=False), 0)                       # per selected point
+        yy = torch.cumsum(_colsum(self.ys, self.ny, self.ldy, self.ys, self.ny, self.ldy, d, 0, self.ny, True,
+                                  dev, host=False), 0)                          # sum_{a<j} |y_a - y_j|
+        si = torch.as_tensor(np.asarray(sizes, dtype=np.int64) - 1, device=dev)
+        k = (si + 1).to(torch.float64)
+        nx = float(self.nx)
+        ed = 2.0 * cross[si] / (nx * k) - 2.0 * xx / (nx * nx) - 2.0 * yy[si] / (k * k)
+        return torch.sqrt(ed)
+
+    def run(self, sizes) -> np.ndarray:
+        return self.launch(sizes).cpu().numpy()
+
+
 def energy_distance_curve(reference_points, sample, idx, sizes) -> np.ndarray:
     """sqrt(energy_distance(reference_points, sample[idx[:k]])) for every k in ``sizes`` -- the
     reference's fit_quality curve (Comparison.ipynb cells 19-23) in one pass."""
-    x = _points(reference_points)
     s = _points(sample)
     sizes = np.asarray(sizes, dtype=np.int64).reshape(-1)
     idx = np.asarray(idx, dtype=np.int64).reshape(-1)
     kmax = int(sizes.max()) if sizes.size else 0
     if kmax > idx.shape[0] or (sizes.size and sizes.min() < 1):
         raise ValueError('sizes must lie in [1, len(idx)]')
-    y = s[idx[:kmax]]
-    _check(x, y)
-    dev = nat.require_device()
-    xs, nx, d, ldx = _soa(x, dev)
-    ys, ny, _, ldy = _soa(y, dev)
-    xx = _colsum(xs, nx, ldx, xs, nx, ldx, d, 0, nx, True, dev).sum()
-    cross = np.cumsum(_colsum(ys, ny, ldy, xs, nx, ldx, d, 0, nx, False, dev))   # per selected point
-    yy = np.cumsum(_colsum(ys, ny, ldy, ys, ny, ldy, d, 0, ny, True, dev))       # sum_{a<j} |y_a - y_j|
-    k = sizes.astype(np.float64)
-    ed = 2.0 * cross[sizes - 1] / (nx * k) - 2.0 * xx / (nx * nx) - 2.0 * yy[sizes - 1] / (k * k)
-    return np.sqrt(ed)
+    return EnergyCurve(reference_points, s[idx[:kmax]]).run(sizes)

@@ -266,6 +266,15 @@ int st_kmat(const double *x_soa, const double *g_soa, const double *weights, int
 int st_distance_colsum(const double *a_soa, int64_t lda, int64_t na, const double *b_soa,
                        int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
                        int32_t triangle, double *out, void *stream);
+/* The same with the B range split over blockIdx.y chunks (>= 2048 blocks in all: a short A -- e.g.
+ * the 1 000 selected points against a 2e5-point validation sample -- still fills the chip): the chunk
+ * partials go to `workspace` (st_distance_workspace_bytes(na, b_begin, b_end) bytes, 16-B aligned;
+ * 0 means no split) and are summed per point in chunk order (deterministic). */
+int64_t st_distance_workspace_bytes(int64_t na, int64_t b_begin, int64_t b_end);
+int st_distance_colsum_ws(const double *a_soa, int64_t lda, int64_t na, const double *b_soa,
+                          int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
+                          int32_t triangle, double *out, void *workspace, int64_t workspace_bytes,
+                          void *stream);
 
 /* ------------------------------------------------------------------------------------------
  * Host-side input preparation -- stein_thinning.thinning._validate_and_standardize (restated at
