@@ -1,0 +1,33 @@
+#!/usr/bin/env bash
+# Host-code sanitizer builds (no GPU involved): the native input preparation
+# (csrc/host_prep.cpp, st_standardize_host) under ASan + UBSan and under TSan (it runs on up to 16
+# threads), and the C-ABI argument validation of the HIP library (capi.hip and the launchers,
+# host side instrumented with -Xarch_host) driven through every entry point's invalid-argument
+# paths -- those return before any HIP call, so they run on a CPU-only machine.
+#   bash scripts/sanitize_host.sh [asan|tsan|abi|all]
+set -eu
+cd "$(dirname "$0")/.."
+OUT=build/sanitize
+mkdir -p $OUT
+CS=gradient-free-mcmc-postprocessing_amd/csrc
+WHAT=${1:-all}
+export ASAN_OPTIONS=detect_leaks=0:abort_on_error=1 UBSAN_OPTIONS=print_stacktrace=1:halt_on_error=1 TSAN_OPTIONS=halt_on_error=1
+if [[ $WHAT == all || $WHAT == asan ]]; then
+  g++ -std=c++17 -O1 -g -fno-omit-frame-pointer -fsanitize=address,undefined -fno-sanitize-recover=all -pthread \
+    -o $OUT/host_prep_asan tools/sanitize/host_prep_check.cpp $CS/host_prep.cpp
+  $OUT/host_prep_asan
+fi
+if [[ $WHAT == all || $WHAT == tsan ]]; then
+  g++ -std=c++17 -O1 -g -fsanitize=thread -pthread -o $OUT/host_prep_tsan tools/sanitize/host_prep_check.cpp $CS/host_prep.cpp
+  $OUT/host_prep_tsan
+fi
+if [[ $WHAT == all || $WHAT == abi ]]; then
+  HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
+  # host side only: each -fsanitize= directly after -Xarch_host (device code is not instrumented)
+  $HIPCC --offload-arch=gfx950 -O1 -g -std=c++17 -ffp-contract=off -Xarch_host -fsanitize=address \
+    -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer \
+    -o $OUT/abi_asan tools/sanitize/abi_invalid_check.cpp $CS/capi.hip $CS/greedy.hip $CS/persistent.hip \
+    $CS/pairwise.hip $CS/proxy.hip $CS/lv.hip $CS/host_prep.cpp
+  $OUT/abi_asan
+fi
+echo sanitize: done

@@ -74,3 +74,27 @@ def test_one_dimensional_input_and_errors():
         se.energy_distance(np.zeros((3, 2)), np.zeros((3, 3)))
     with pytest.raises(ValueError):
         se.energy_distance_curve(x, y, np.arange(100), [101])
+
+
+@pytest.mark.parametrize('d', [3, 4, 11])
+def test_chunked_ranges_against_oracle(d):
+    """A short A against a long B (the selection against the validation sample) and a long
+    triangle: both split over blockIdx.y chunks of B with the workspace reduction; the same value
+    as the oracle, and the chunked column sums equal the unsplit kernel's to rounding."""
+    from stein_thinning import _native as nat
+    rng = np.random.default_rng(d + 40)
+    x = rng.normal(size=(6011, d))
+    y = rng.normal(size=(301, d)) * 0.7 + 0.1
+    assert nat.lib().st_distance_workspace_bytes(301, 0, 6011) > 0
+    np.testing.assert_allclose(se.energy_distance(x, y), o.energy_distance(x, y), rtol=1e-12)
+    sizes = np.array([1, 5, 150, 301])
+    want = [np.sqrt(o.energy_distance(x, y[:k])) for k in sizes]
+    np.testing.assert_allclose(se.energy_distance_curve(x, y, np.arange(301), sizes), want, rtol=1e-10)
+    dev = torch.device('cuda', 0)
+    ys, ny, _, ldy = se._soa(y, dev)
+    xs, nx, _, ldx = se._soa(x, dev)
+    split = se._colsum(ys, ny, ldy, xs, nx, ldx, d, 0, nx, False, dev)
+    whole = torch.zeros(ny, dtype=torch.float64, device=dev)
+    nat.check(nat.lib().st_distance_colsum(nat.ptr(ys), ldy, ny, nat.ptr(xs), ldx, nx, d, 0, nx, 0, nat.ptr(whole),
+                                           nat.stream_handle()), 'st_distance_colsum')
+    np.testing.assert_allclose(split, whole.cpu().numpy(), rtol=1e-13)
