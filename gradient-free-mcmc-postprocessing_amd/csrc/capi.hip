@@ -352,6 +352,29 @@ int st_greedy_step_exchange(const double* x_soa, const double* g_soa, const doub
                      "rank exchange launch");
 }
 
+int64_t st_kde_workspace_bytes(int64_t m, int32_t d) {
+    if (m < 0 || d < 1 || d > st::kMaxDim) return -1;
+    return st::kde_workspace_bytes(m, d);
+}
+
+int st_kde_logpdf_grad(const double* p_soa, int64_t ldp, int64_t n, const double* log_weights,
+                       double log_weight_uniform, const double* q_soa, int64_t ldq, int64_t m, int32_t d,
+                       double log_norm, const double* whiten, double* log_q_out, double* grad_out,
+                       void* workspace, int64_t workspace_bytes, void* stream) {
+    if (m == 0) return ST_OK;
+    if (!p_soa || !q_soa || !whiten || !log_q_out || !grad_out) return fail(ST_ERR_INVALID, "NULL pointer");
+    if (d < 1 || d > st::kMaxDim) return fail(ST_ERR_UNSUPPORTED, "unsupported d = %d", d);
+    if (n < 1 || m < 0 || ldp < n || ldq < m) return fail(ST_ERR_INVALID, "bad sizes (need n >= 1, ld >= count)");
+    if ((m + 255) / 256 > 0x7FFFFFFFll) return fail(ST_ERR_UNSUPPORTED, "m too large");
+    if (workspace_bytes < st::kde_workspace_bytes(m, d) || (st::kde_workspace_bytes(m, d) > 0 && !workspace))
+        return fail(ST_ERR_INVALID, "workspace too small (%lld < %lld)", (long long)workspace_bytes,
+                    (long long)st::kde_workspace_bytes(m, d));
+    return hip_check(st::launch_kde(p_soa, ldp, n, log_weights, log_weight_uniform, q_soa, ldq, m, d, log_norm,
+                                    whiten, log_q_out, grad_out, static_cast<double*>(workspace),
+                                    static_cast<hipStream_t>(stream)),
+                     "kde launch");
+}
+
 int st_proxy_logpdf_grad(const double* x, int64_t n, int32_t d, const double* loc,
                          const double* whiten, const double* precision, double df, double c_log,
                          double* log_q_out, double* grad_out, void* stream) {

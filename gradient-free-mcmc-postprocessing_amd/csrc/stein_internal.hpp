@@ -87,6 +87,10 @@ struct ProxyArgs {
     double* grad;        // row-major (n, d)
 };
 int64_t proxy_lds_bytes(int d);
+int64_t kde_workspace_bytes(int64_t m, int d);
+hipError_t launch_kde(const double* p, int64_t ldp, int64_t n, const double* logw, double logw0,
+                      const double* q, int64_t ldq, int64_t m, int d, double log_norm, const double* L,
+                      double* log_q, double* grad, double* ws, hipStream_t s);
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s);
 int proxy_tune(int value);   // st_tune key 7
 

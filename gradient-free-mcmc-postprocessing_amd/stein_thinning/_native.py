@@ -82,6 +82,9 @@ SIGNATURES = {
     'st_lv_log_density_workspace_bytes': (_i64, [_i64, _i32]),
     'st_lv_log_target_density': (ctypes.c_int, [_c_dp, _c_dp, _i64, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _f64,
                                                 _f64, _i64, _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
+    'st_kde_workspace_bytes': (_i64, [_i64, _i32]),
+    'st_kde_logpdf_grad': (ctypes.c_int, [_c_dp, _i64, _i64, _c_dp, _f64, _c_dp, _i64, _i64, _i32, _f64, _c_dp,
+                                          _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
     'st_proxy_logpdf_grad': (ctypes.c_int, [_c_dp, _i64, _i32, _c_dp, _c_dp, _c_dp, _f64, _f64, _c_dp,
                                             _c_dp, _c_dp]),
 }

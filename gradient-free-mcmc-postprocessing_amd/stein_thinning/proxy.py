@@ -10,7 +10,12 @@ The reference builds the proxy q of ``thin_gf`` on the host before every gradien
   ``log_q = scipy.stats.multivariate_t.logpdf(sample, loc, shape, df)``, ``gradient_q =
   t_grad_log_pdf(sample, loc, shape, df)``; both with ``range_cap=200``.
 
-That is O(n d^2) per proxy (C5: n = 5e5, d = 50).  Here the d x d factors are computed on the host
+* the KDE proxy of ``Gaussian_mixture.ipynb`` cells 42-48 (and the weighted KDE of cell 51):
+  ``kde = jax.scipy.stats.gaussian_kde(sample.T, bw_method='silverman'[, weights=w])``,
+  ``log_q = kde.logpdf(sample.T)``, ``gradient_q`` = jax.grad of it at every row
+  (``kde_proxy``; O(n^2 d): csrc/kde.hip, ``st_kde_logpdf_grad``).
+
+The parametric proxies are O(n d^2) per proxy (C5: n = 5e5, d = 50).  Here the d x d factors are computed on the host
 exactly as scipy does (``_PSD``: eigh, pseudo-inverse square root; ``np.linalg.inv``; the scalar
 constants in scipy's operation order) and the per-row work runs in one HIP kernel
 (``st_proxy_logpdf_grad``, csrc/proxy.hip).  The per-row dot products are summed in a different
@@ -120,6 +125,78 @@ def student_t_proxy(sample, loc, shape, df: float) -> Tuple[np.ndarray, np.ndarr
     t = 0.5 * (df + d)
     c_log = gammaln(t) - gammaln(0.5 * df) - d / 2. * np.log(df * np.pi) - 0.5 * psd.log_pdet
     return _device_eval(x, loc, psd.U, precision, df, float(c_log))
+
+
+def kde_factors(dataset, bw_method='silverman', weights=None):
+    """The constructor arithmetic of jax.scipy.stats.gaussian_kde (= scipy.stats.gaussian_kde) on an
+    (n, d) dataset: normalised weights, n_eff, the bandwidth factor ('scott', 'silverman' or a
+    scalar), the weighted data covariance, the precision inv(cov) / factor^2 and its lower
+    Cholesky factor L (the kernel evaluation whitens with it: points @ L), log_norm =
+    sum(log diag L) - d/2 log(2 pi).  Returns (weights, L, log_norm)."""
+    x = np.asarray(dataset, dtype=np.float64)
+    if x.ndim == 1:
+        x = x[:, None]
+    n, d = x.shape
+    if n < 2:
+        raise ValueError('a KDE needs at least two data points')
+    w = np.full(n, 1.0 / n) if weights is None else np.asarray(weights, dtype=np.float64).reshape(-1)
+    if w.shape != (n,):
+        raise ValueError(f'weights must have length {n}')
+    w = w / np.sum(w)
+    neff = 1.0 / np.sum(w ** 2)
+    if bw_method is None or bw_method == 'scott':
+        factor = np.power(neff, -1.0 / (d + 4))
+    elif bw_method == 'silverman':
+        factor = np.power(neff * (d + 2) / 4.0, -1.0 / (d + 4))
+    elif np.isscalar(bw_method) and not isinstance(bw_method, str):
+        factor = float(bw_method)
+    else:
+        raise ValueError("bw_method must be 'scott', 'silverman' or a scalar")
+    cov = np.atleast_2d(np.cov(x.T, rowvar=1, bias=False, aweights=w))
+    inv_cov = np.linalg.inv(cov) / factor ** 2
+    L = np.linalg.cholesky(inv_cov)
+    log_norm = float(np.sum(np.log(np.diag(L))) - 0.5 * d * np.log(2 * np.pi))
+    return w, L, log_norm
+
+
+def kde_proxy(sample, points=None, bw_method='silverman', weights=None) -> Tuple[np.ndarray, np.ndarray]:
+    """(log_q, gradient_q) of the Gaussian KDE of ``sample`` at ``points`` (default: the sample
+    itself) -- ``gaussian_kde(sample.T, bw_method, weights).logpdf(points.T)`` and its gradient, as
+    Gaussian_mixture.ipynb cells 46-48 / 51 compute them for thin_gf.  The O(n m d) pair sums run
+    on the GPU (st_kde_logpdf_grad); agrees with the restatement to fp64 rounding (the
+    logsumexp and the softmax-weighted sums are sequential here, pairwise in NumPy)."""
+    import torch
+    from .device import padded_ld
+    data = np.asarray(sample, dtype=np.float64)
+    data = data[:, None] if data.ndim == 1 else data
+    pts = data if points is None else np.asarray(points, dtype=np.float64)
+    pts = pts[:, None] if pts.ndim == 1 else pts
+    n, d = data.shape
+    if pts.ndim != 2 or pts.shape[1] != d:
+        raise ValueError(f'points must be (m, {d})')
+    m = pts.shape[0]
+    w, L, log_norm = kde_factors(data, bw_method, weights)
+    dev = nat.require_device()
+    log_q = torch.empty(max(m, 1), dtype=torch.float64, device=dev)
+    grad = torch.empty((max(m, 1), d), dtype=torch.float64, device=dev)
+    if m:
+        def soa(a):
+            ld = padded_ld(a.shape[0])
+            t = torch.zeros((d, ld), dtype=torch.float64, device=dev)
+            t[:, :a.shape[0]] = torch.from_numpy(np.ascontiguousarray((a @ L).T)).to(dev)   # whitened: a @ L
+            return t, ld
+        p_t, ldp = soa(data)
+        q_t, ldq = soa(pts)
+        uniform = weights is None
+        logw = None if uniform else torch.from_numpy(np.log(w)).to(dev)
+        lt = torch.from_numpy(np.ascontiguousarray(L)).to(dev)
+        wsb = int(nat.lib().st_kde_workspace_bytes(m, d))
+        ws = torch.empty(max(wsb // 8, 2), dtype=torch.float64, device=dev)
+        nat.check(nat.lib().st_kde_logpdf_grad(nat.ptr(p_t), ldp, n, nat.ptr(logw), float(np.log(1.0 / n)),
+                                               nat.ptr(q_t), ldq, m, d, log_norm, nat.ptr(lt), nat.ptr(log_q),
+                                               nat.ptr(grad), nat.ptr(ws), ws.numel() * 8, nat.stream_handle()),
+                  'st_kde_logpdf_grad')
+    return log_q[:m].cpu().numpy(), grad[:m].cpu().numpy()
 
 
 def gaussian_thin(sample, log_p, mean, cov, thinned_size: int, range_cap: Optional[float] = 200) -> np.ndarray:

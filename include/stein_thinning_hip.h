@@ -189,6 +189,22 @@ int st_proxy_logpdf_grad(const double *x, int64_t n, int32_t d, const double *lo
                          double *log_q_out, double *grad_out, void *stream);
 
 /* ------------------------------------------------------------------------------------------
+ * KDE proxy -- replaces jax.scipy.stats.gaussian_kde(sample.T, bw_method, weights).logpdf and its
+ * jax.grad as the reference's Gaussian-mixture study feeds them to thin_gf (Gaussian_mixture.ipynb
+ * cells 42-48, 51).  Whitened data p = x L (n points, SoA (d, ldp)) and queries q = y L (m points,
+ * SoA (d, ldq)), L = cholesky(KDE precision) (HOST-computed; `whiten` = L on the DEVICE, (d, d)
+ * row-major); log_weights (n, device) or NULL for the uniform log_weight_uniform:
+ *   log_q[j] = logsumexp_i(log w_i + log_norm - |p_i - q_j|^2 / 2),
+ *   grad[j]  = (sum_i softmax_i(.) p_i - q_j) L^T   (row-major (m, d)).
+ * workspace: st_kde_workspace_bytes(m, d) bytes (0 for d <= 8).
+ * ---------------------------------------------------------------------------------------- */
+int64_t st_kde_workspace_bytes(int64_t m, int32_t d);
+int st_kde_logpdf_grad(const double *p_soa, int64_t ldp, int64_t n, const double *log_weights,
+                       double log_weight_uniform, const double *q_soa, int64_t ldq, int64_t m, int32_t d,
+                       double log_norm, const double *whiten, double *log_q_out, double *grad_out,
+                       void *workspace, int64_t workspace_bytes, void *stream);
+
+/* ------------------------------------------------------------------------------------------
  * Lotka-Volterra inputs, batched over n parameter points (one RK45 integration per point, scipy's
  * solve_ivp algorithm step for step -- code/src/lotka_volterra.py):
  *   st_lv_grad_log_posterior: grad_out (n, 4) row-major = grad_log_posterior(theta) of

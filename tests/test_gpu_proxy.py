@@ -129,3 +129,41 @@ def test_matrix_core_variants_match_scipy(mode, d):
     _close(gq, wg)
     _close(ltq, tl)
     _close(gtq, tg)
+
+
+@pytest.mark.parametrize('d', [1, 2, 3, 4, 8, 9, 12])
+@pytest.mark.parametrize('weighted', [False, True])
+def test_kde_proxy_matches_restatement(d, weighted):
+    """KDE proxy (csrc/kde.hip) against oracle.proxy_numpy.kde_proxy (jax gaussian_kde restated):
+    log q and grad log q to fp64 rounding, at the sample itself and at other points; the
+    compile-time-d (d <= 8) and runtime-d kernels; uniform and weighted KDEs (cell 51)."""
+    x, mean, cov = _case(1501, d, 31 * d + weighted)
+    w = np.exp(-0.3 * np.sum((x - mean) ** 2, axis=1)) if weighted else None
+    lq, gq = proxy.kde_proxy(x, bw_method='silverman', weights=w)
+    wl, wg = op.kde_proxy(x, bw_method='silverman', weights=w)
+    _close(lq, wl)
+    _close(gq, wg)
+    y = x[:257] * 1.1 + 0.05
+    lq, gq = proxy.kde_proxy(x, y, bw_method='scott')
+    wl, wg = op.kde_proxy(x, y, bw_method='scott')
+    _close(lq, wl)
+    _close(gq, wg)
+
+
+def test_kde_gradient_free_curves_on_gpu(gm, curves):
+    """Gaussian_mixture.ipynb cells 42-48 end to end on the GPU: the KDE proxy, thin_gf (1 000
+    points, 'med'), calculate_ksd and the energy-distance curve -- against the report's gf_kde
+    curves (report/figures/gaussian-mixture-comparison.pdf) at the PDF's precision."""
+    from stein_thinning import energy as se
+    from stein_thinning import stein as ss
+    from stein_thinning import thinning as st
+    sample, sample2, logpdf, score = gm
+    log_q, gq = proxy.kde_proxy(sample, bw_method='silverman')
+    idx = st.thin_gf(sample, logpdf(sample), log_q, gq, 1000, preconditioner='med')
+    integrand = st._make_stein_integrand(sample, score(sample))
+    ks = ss.ksd(integrand.reindex(idx), idx.shape[0])
+    c = np.array(curves['ksd/gf_kde'])
+    np.testing.assert_allclose(ks[c[:, 0].astype(int) - 1], c[:, 1], rtol=1e-7)
+    c = np.array(curves['ed/gf_kde'])
+    got = se.energy_distance_curve(sample2, sample, idx, c[:, 0].astype(int))
+    np.testing.assert_allclose(got, c[:, 1], rtol=1.5e-8)

@@ -111,6 +111,24 @@ def test_f3_energy_distance_curves(gm_runs, curves):
         np.testing.assert_allclose(ed, c[:, 1], rtol=CURVE_RTOL)
 
 
+def test_f3_kde_proxy_curves(gm_runs, curves):
+    """The gradient-free KDE curves of report/figures/gaussian-mixture-comparison.pdf
+    (Gaussian_mixture.ipynb cells 42-48: jax gaussian_kde, silverman, thin_gf with 'med', 1 000
+    points) reproduced by oracle.proxy_numpy.kde_proxy (fp64) + the NumPy thin_gf: KSD and energy
+    distance at the PDF's precision.  The reference evaluated the KDE in JAX's default fp32; the
+    selection does not depend on the difference."""
+    from oracle import proxy_numpy as op
+    s, s2 = gm_runs['sample'], gm_runs['sample2']
+    log_q, gq = op.kde_proxy(s, bw_method='silverman')
+    idx = o.thin_gf(s, gm_runs['log_p'], log_q, gq, 1000, preconditioner='med')
+    ks = o.calculate_ksd(s, gm_runs['gradient'], idx)
+    c = np.array(curves['ksd/gf_kde'])
+    np.testing.assert_allclose(ks[c[:, 0].astype(int) - 1], c[:, 1], rtol=CURVE_RTOL)
+    c = np.array(curves['ed/gf_kde'])[::13]
+    ed = np.array([np.sqrt(o.energy_distance(s[idx[:k]], s2)) for k in c[:, 0].astype(int)])
+    np.testing.assert_allclose(ed, c[:, 1], rtol=CURVE_RTOL)
+
+
 def test_f4_kmat_extremes(gm, golden):
     sample, _, _, _ = gm
     f = golden['F2_gaussian_mixture']
