@@ -21,7 +21,7 @@
 // candidate's row from the replicated inputs, and picks the global winner in np.argmin order.
 // No host round trip and no collective launch per step.
 // Arithmetic per pair: K2's (stein_math.hpp) or, when the block's rows and the winner lie in the
-// guarded range, its division/sqrt-light form that returns the same bits (fast_div / fast_sqrt):
+// guarded range, its division/sqrt-light form that returns the same bits (finish_pair_fast):
 // results are bit-identical to st_greedy's launch-per-step path and to the C bit model.
 #include <type_traits>
 

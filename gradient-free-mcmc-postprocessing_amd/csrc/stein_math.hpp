@@ -19,22 +19,21 @@ namespace st {
 
 // qf^1.5 and qf^2.5 correctly rounded to ~2^-100 (then rounded once), from s = sqrt(qf) (correctly
 // rounded) and its exact residual e = qf - s^2 (fma).  sqrt(qf) = s + e/(2s) + O(2^-106 s), and the
-// correction terms q * e/(2s) and q^2 * e/(2s) equal (s/2) e and (q s/2) e to 2^-53 relative of a term
-// that is itself ~2^-53 of the result -- so no division is needed.
+// correction term q * e/(2s) equals (s/2) e to 2^-53 relative of a term that is itself ~2^-53 of the
+// result -- so no division is needed: q^1.5 = hi + lo (double-double, hi = fl(q s)).  q^2.5 is
+// q (hi + lo) as a second double-double product (q hi exactly by fma, + q lo), rounded once.  An
+// overflowing power is +inf (the double-double tail would turn it into inf - inf).
 __device__ __forceinline__ void pow_15_25(double q, double& p15, double& p25, double& s) {
     s = __builtin_sqrt(q);
     const double e = __builtin_fma(-s, s, q);
     const double hi = q * s;
     double lo = __builtin_fma(q, s, -hi);
     lo = __builtin_fma(0.5 * s, e, lo);
-    p15 = hi + lo;
-    const double q2 = q * q;
-    const double q2lo = __builtin_fma(q, q, -q2);
-    const double hi2 = q2 * s;
-    double lo2 = __builtin_fma(q2, s, -hi2);
-    lo2 = __builtin_fma(q2lo, s, lo2);
-    lo2 = __builtin_fma(0.5 * hi, e, lo2);
-    p25 = hi2 + lo2;
+    p15 = __builtin_isinf(hi) ? hi : hi + lo;
+    const double hi2 = q * hi;
+    double lo2 = __builtin_fma(q, hi, -hi2);
+    lo2 = __builtin_fma(q, lo, lo2);
+    p25 = __builtin_isinf(hi2) ? hi2 : hi2 + lo2;
 }
 
 __device__ __forceinline__ double finish_pair(double qs, double t1s, double t2s, double t3s,
@@ -54,13 +53,12 @@ __device__ __forceinline__ double finish_pair(double qs, double t1s, double t2s,
 // a normal number far from the limits: differences are 0 or >= 2^-112 (multiples of 2^-112),
 // per-k products 0 or in [2^-344, 2^242], their sums 0 or >= 2^-396 (multiples of the smallest
 // ulp), qf in [1, 2^185], p25 <= 2^463, and every quotient is normal.  In that range
-//   * the compiler's IEEE f64 division sequence (v_div_scale x2, v_rcp, 2 Newton steps, v_mul,
-//     residual fma, v_div_fmas, v_div_fixup) never scales: div_scale returns its operand with
-//     VCC = 0, div_fmas is a plain fma and div_fixup returns the quotient unchanged;
+//   * the IEEE f64 division a / b needs no scaling and no special-case fix-up: the quotient is
+//     q0 + rem r rounded once with r = RN(1/b) (div_by_recip), all intermediates normal;
 //   * its sqrt sequence (scale-if-below-2^-767, v_rsq, Goldschmidt + 2 residual corrections,
 //     +0/-0/+inf class fix-up) never scales and never takes the fix-up;
 // (|k| < 2^190 there, so the running-sum update A + 2k may also be the single fma(2, k, A): 2k is
-// exact.)  So fast_div / fast_sqrt below -- the same sequences without those steps -- return the same bits
+// exact.)  So fast_sqrt and div_by_recip below (no scaling / fix-up steps) return the same bits
 // as '/' and sqrt, correctly rounded.  The only deviations are signs of zero: a -0 numerator gives
 // +0 instead of -0 in t1/t3, and t3s drops the leading "0.0 +".  k = fl(fl(t1 + t2) + t3) is
 // unaffected because t2 = fl(tr + t2s) / p15 is never -0 (tr > 0), so a zero t1 or t3 only ever
@@ -77,7 +75,9 @@ __device__ __forceinline__ int fast_range_ok(double v) {   // 1 / 0, branch-free
     return (int)(a == 0.0) | ((int)(a >= 0x1p-60) & (int)(a <= 0x1p60));
 }
 
-__device__ __forceinline__ double fast_sqrt(double x) {   // x in [1, 2^185]
+// sqrt of x in [1, 2^185], correctly rounded (the compiler's sequence without its scaling and
+// class fix-up); h ~ 1 / (2 sqrt x) to ~2^-48 comes out as a by-product
+__device__ __forceinline__ double fast_sqrt(double x, double& h_out) {
     double g = x * __builtin_amdgcn_rsq(x);
     double h = __builtin_amdgcn_rsq(x) * 0.5;
     const double r = __builtin_fma(-h, g, 0.5);
@@ -86,24 +86,38 @@ __device__ __forceinline__ double fast_sqrt(double x) {   // x in [1, 2^185]
     double dd = __builtin_fma(-g, g, x);
     g = __builtin_fma(dd, h, g);
     dd = __builtin_fma(-g, g, x);
+    h_out = h;
     return __builtin_fma(dd, h, g);
 }
 
-__device__ __forceinline__ double fast_div(double a, double b) {   // b in [1, 2^463], a/b normal or 0
-    double r = __builtin_amdgcn_rcp(b);
-    double e = __builtin_fma(-b, r, 1.0);
-    r = __builtin_fma(r, e, r);
-    e = __builtin_fma(-b, r, 1.0);
-    r = __builtin_fma(r, e, r);
+// RN(1/b) from a seed y0 within ~2^-48 of 1/b: two Newton steps (error 2^-96, then 2^-150 before the
+// final rounding -- far inside the >= 2^-106 relative gap between 1/b and any rounding midpoint, so
+// the result is the correctly rounded reciprocal whatever the seed's exact bits)
+__device__ __forceinline__ double recip2(double b, double y0) {
+    double e = __builtin_fma(-b, y0, 1.0);
+    double y = __builtin_fma(y0, e, y0);
+    e = __builtin_fma(-b, y, 1.0);
+    return __builtin_fma(y, e, y);
+}
+
+// a / b from r = RN(1/b): q0 = fl(a r) is within an ulp of a/b, the remainder a - b q0 is exact, and
+// q0 + rem r rounded once is the correctly rounded quotient (Markstein) -- the IEEE result of '/'
+__device__ __forceinline__ double div_by_recip(double a, double b, double r) {
     const double q = a * r;
     const double rem = __builtin_fma(-b, q, a);
     return __builtin_fma(rem, r, q);
 }
 
+// Fast range (see above): the same bits as finish_pair.  The three reciprocals need no v_rcp_f64
+// (a quarter-rate transcendental with 2^-24 accuracy: ~3.3 fma issue slots each at two waves per
+// SIMD, profiles/r02_trans_rate.log): 1/s is seeded by the sqrt's own h (2h ~ 1/s to 2^-48), and
+// 1/p15, 1/p25 by rs^3, rs^5 (within ~2^-50 of them since p15, p25 are the correctly rounded
+// s^3-, s^5-sized powers); each seed is refined by recip2 to the correctly rounded reciprocal.
 __device__ __forceinline__ double finish_pair_fast(double qs, double t1s, double t2s, double t3s,
                                                    double tr) {
     const double q = 1.0 + qs;
-    const double s = fast_sqrt(q);
+    double h;
+    const double s = fast_sqrt(q, h);
     const double e = __builtin_fma(-s, s, q);
     // e is a multiple of 2^-104 (s >= 1), so 0.5*e is exact and (0.5*s)*e == s*(0.5*e) exactly
     const double he = 0.5 * e;
@@ -111,16 +125,18 @@ __device__ __forceinline__ double finish_pair_fast(double qs, double t1s, double
     double lo = __builtin_fma(q, s, -hi);
     lo = __builtin_fma(s, he, lo);
     const double p15 = hi + lo;
-    const double q2 = q * q;
-    const double q2lo = __builtin_fma(q, q, -q2);
-    const double hi2 = q2 * s;
-    double lo2 = __builtin_fma(q2, s, -hi2);
-    lo2 = __builtin_fma(q2lo, s, lo2);
-    lo2 = __builtin_fma(hi, he, lo2);
+    const double hi2 = q * hi;
+    double lo2 = __builtin_fma(q, hi, -hi2);
+    lo2 = __builtin_fma(q, lo, lo2);
     const double p25 = hi2 + lo2;
-    const double t1 = fast_div(-3.0 * t1s, p25);
-    const double t2 = fast_div(tr + t2s, p15);
-    const double t3 = fast_div(t3s, s);
+    const double rs = recip2(s, h + h);
+    const double rs2 = rs * rs;
+    const double rs3 = rs2 * rs;
+    const double r15 = recip2(p15, rs3);
+    const double r25 = recip2(p25, rs3 * rs2);
+    const double t1 = div_by_recip(-3.0 * t1s, p25, r25);
+    const double t2 = div_by_recip(tr + t2s, p15, r15);
+    const double t3 = div_by_recip(t3s, s, rs);
     return (t1 + t2) + t3;
 }
 

@@ -52,22 +52,20 @@ static double pairwise_sum(const double *v, int64_t n) {
 }
 
 /* correctly rounded (to ~2^-100, then rounded once) qf^1.5, qf^2.5 from s = sqrt(qf) and its exact
- * residual e = qf - s^2: the correction terms q*e/(2s), q^2*e/(2s) are evaluated as (s/2)*e and
- * (q*s/2)*e (equal to 2^-53 relative of a 2^-53-relative term) -- the kernels' exact op sequence */
+ * residual e = qf - s^2: the correction term q*e/(2s) is evaluated as (s/2)*e (equal to 2^-53
+ * relative of a 2^-53-relative term); q^1.5 = hi + lo as a double-double, q^2.5 = q * (hi + lo) as a
+ * second double-double product -- the kernels' exact op sequence (an overflowing power is +inf) */
 static void pow_15_25(double q, double *p15, double *p25, double *sq) {
     double s = sqrt(q);
     double e = fma(-s, s, q);
     double hi = q * s;
     double lo = fma(q, s, -hi);
     lo = fma(0.5 * s, e, lo);
-    *p15 = hi + lo;
-    double q2 = q * q;
-    double q2lo = fma(q, q, -q2);
-    double hi2 = q2 * s;
-    double lo2 = fma(q2, s, -hi2);
-    lo2 = fma(q2lo, s, lo2);
-    lo2 = fma(0.5 * hi, e, lo2);
-    *p25 = hi2 + lo2;
+    *p15 = isinf(hi) ? hi : hi + lo;
+    double hi2 = q * hi;
+    double lo2 = fma(q, hi, -hi2);
+    lo2 = fma(q, lo, lo2);
+    *p25 = isinf(hi2) ? hi2 : hi2 + lo2;
     *sq = s;
 }
 
@@ -234,6 +232,14 @@ int sr_greedy_mt(const double *x, const double *g, const double *w, int64_t n, i
     free(th);
     free(args);
     return rc;
+}
+
+/* the bit model's powers for a vector of qf values (tests: against Decimal-exact powers) */
+void sr_pow_15_25(const double *q, int64_t n, double *p15, double *p25) {
+    for (int64_t i = 0; i < n; i++) {
+        double s;
+        pow_15_25(q[i], &p15[i], &p25[i], &s);
+    }
 }
 
 /* pair values out[p] = k(i1[p], i2[p]) with weights fl(fl(k*w_i1)*w_i2) */

@@ -28,6 +28,8 @@ def lib():
         L.sr_greedy_mt.restype = ctypes.c_int
         L.sr_greedy_mt.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp,
                                    ctypes.c_int]
+        L.sr_pow_15_25.restype = None
+        L.sr_pow_15_25.argtypes = [dp, i64, dp, dp]
         L.sr_pairs.restype = ctypes.c_int
         L.sr_pairs.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, dp, i64, dp]
         _lib = L
@@ -80,3 +82,10 @@ def pairs(x, g, w, l, tr, i1, i2):
     rc = lib().sr_pairs(_p(x), _p(g), _p(w), x.shape[0], x.shape[1], l, tr, _p(i1), _p(i2), i1.shape[0], _p(out))
     assert rc == 0
     return out
+
+
+def pow_15_25(q):
+    q = np.ascontiguousarray(q, dtype=np.float64)
+    p15, p25 = np.empty_like(q), np.empty_like(q)
+    lib().sr_pow_15_25(_p(q), q.shape[0], _p(p15), _p(p25))
+    return p15, p25

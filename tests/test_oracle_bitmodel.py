@@ -140,3 +140,23 @@ def test_threaded_bit_model_equals_sequential(d, gf):
         idx, A = oracle_c.greedy_mt(x, g, w, 0.7, 0.7 * d, m, nt)
         np.testing.assert_array_equal(idx, want_idx)
         assert np.array_equal(A, want_A, equal_nan=True)
+
+
+def test_bit_model_powers_are_correctly_rounded():
+    """qf^1.5 and qf^2.5 of the bit model (double-double to ~2^-105, q^2.5 as q times the q^1.5
+    pair, then rounded once) against 80-digit Decimal powers: correctly rounded on 20 000
+    log-uniform qf in [1, 2^120]; at values built to sit within 2^-106 of a rounding midpoint
+    (qf just below a power of four: (4 - 2^-51)^1.5 = 8 - 1.5 2^-50 + 3 2^-106) the double-double
+    cannot decide and the result may be the other neighbour -- within one ulp, as NumPy's own pow."""
+    rng = np.random.default_rng(7)
+    q = np.exp2(rng.uniform(0, 120, size=20_000)) * (1 + rng.uniform(0, 1e-3, size=20_000))
+    p15, p25 = oracle_c.pow_15_25(q)
+    want15 = np.array([_cr_pow(v, 1.5) for v in q])
+    want25 = np.array([_cr_pow(v, 2.5) for v in q])
+    assert np.array_equal(p15, want15), np.flatnonzero(p15 != want15)[:5]
+    assert np.array_equal(p25, want25), np.flatnonzero(p25 != want25)[:5]
+    edge = np.array([1.0, np.nextafter(1.0, 2.0), 2.0, 4.0, np.nextafter(4.0, 0.0), 2.0 ** 100])
+    e15, e25 = oracle_c.pow_15_25(edge)
+    for got, e in ((e15, 1.5), (e25, 2.5)):
+        want = np.array([_cr_pow(v, e) for v in edge])
+        assert np.all(np.abs(got - want) <= np.spacing(want))
