@@ -235,6 +235,15 @@ def _max_over_ranks(values, dev):
     return [float(v) for v in t.tolist()]
 
 
+def pmc_traffic(key: str):
+    """HBM bytes per launch of a workload's dominant kernel from the committed PMC summary
+    (profiles/pmc_traffic.json, written by tools/summarize_pmc.py from rocprofv3 FETCH_SIZE /
+    WRITE_SIZE passes with the gfx950 corrections), or None when no pass was recorded."""
+    path = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
+    rec = (json.load(open(path)) if os.path.exists(path) else {}).get(key)
+    return round(rec['hbm_bytes_per_launch']) if rec else None
+
+
 def algorithmic_flop_per_pair(d: int, gf: bool) -> int:
     """Algorithmic fp64 work of one Stein-kernel pair, SURVEY.md section 8(d): 12 d + 40 flop
     (isotropic Gamma^-1; the per-coordinate products and sums of vfk0_imq,
@@ -365,11 +374,11 @@ def main():
         # algorithmic work per pair: what `frac` is priced on
         flop_per_pair = algorithmic_flop_per_pair(d, gf)
         # what the persistent kernel's hot loop actually issues, counted in its ISA
-        # (greedy_persistent<4,false,8,512>): 38 v_mul_f64 + 26 v_add_f64 + 33 v_fma/v_fmac_f64
-        # + 3 v_rcp_f64 + 1 v_rsq_f64 = 101 fp64 VALU instructions, 134 flop (fma = 2); each further
-        # coordinate adds 13; the gradient-free weights add 2 mul
+        # (greedy_persistent<4,false,8,512>; tools/pair_rate.hip): 40 v_mul_f64 + 28 v_add_f64 + 31
+        # v_fma/v_fmac_f64 + 1 v_rsq_f64 + 1 v_cmp_f64 = 101 fp64 VALU instructions, 130 flop (fma = 2);
+        # each further coordinate adds 13; the gradient-free weights add 2 mul
         instr_per_pair = 101 + 13 * (d - 4) + (2 if gf else 0)
-        issue_flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0)
+        issue_flop_per_pair = 130 + 13 * (d - 4) + (2 if gf else 0)
         pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
         pmc_rec = json.load(open(pmc)) if os.path.exists(pmc) else {}
         if persistent:
@@ -550,7 +559,8 @@ def main_energy(args):
                        'pairs_per_step': int(pairs), 'ed_at_1000': float(got[-1]),
                        'parallelism': f'replicas x{world}' if world > 1 else 'single-gpu'},
             'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
-                         'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': None,
+                         'frac': round(tflops / FP64_VALU_PEAK_TFS, 4),
+                         'traffic': pmc_traffic('energy') if world == 1 else None,
                          'kernel': f'dist_colsum_kernel<{d}> (+ reduce / cumsum)', 'step_median_us': round(step_s * 1e6, 1),
                          'flop_per_pair': flop_pair,
                          'note': 'per pair: d differences, squares and sums, one IEEE sqrt (a ~10-instruction '
@@ -669,7 +679,8 @@ def main_ksd(args):
                        'parallelism': f'triangle rows x{world}, RCCL all-reduce of the n-vector' if world > 1
                        else 'single-gpu'},
             'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
-                         'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': None,
+                         'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4),
+                         'traffic': pmc_traffic('ksd_' + ('c4' if args.ksd_full else 'c2')) if world == 1 else None,
                          'kernel': f'ksd_colsum_kernel<{d},{str(gf).lower()}>', 'kernel_avg_us': round(colsum_s * 1e6, 1),
                          'flop_per_pair': flop_per_pair,
                          'flop_per_pair_source': 'SURVEY.md 8(d): 12 d + 40 (+2 gradient-free) + 1 accumulate',
@@ -763,7 +774,8 @@ def main_proxy(args):
                   'frac': round(gbs / HBM_PEAK_GBS, 4)} if hbm_bound else
                  {'bound': 'mfma' if mfma else 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,
                   'unit': 'TFLOP/s', 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4)}),
-                traffic=None, kernel=(('proxy_mfma_buf_kernel<4,14>' if args.proxy_mode in (0, 4) and d % 2 == 0
+                traffic=pmc_traffic('proxy_' + args.proxy_kind) if world == 1 and args.proxy_mode == 0 else None,
+                kernel=(('proxy_mfma_buf_kernel<4,14>' if args.proxy_mode in (0, 4) and d % 2 == 0
                                        else 'proxy_mfma_stream_kernel<4,14>' if args.proxy_mode in (0, 3, 4)
                                        else 'proxy_mfma_kernel (LDS-tiled)') if mfma else 'proxy_kernel'),
                 kernel_avg_us=round(kern_s * 1e6, 1), flop_per_row=flop_row, bytes_per_row=bytes_row,
@@ -853,7 +865,7 @@ def main_lv(args):
                                    'rtol 1e-3 / atol 1e-6', 'n': n,
                        'parallelism': f'point blocks x{world}' if world > 1 else 'single-gpu'},
             'roofline': {'bound': 'latency', 'achieved': None, 'peak': None, 'unit': None, 'frac': None,
-                         'traffic': None, 'kernel': 'lv_kernel<10>', 'kernel_avg_us': round(kern_s * 1e6, 1),
+                         'traffic': pmc_traffic('lv') if world == 1 else None, 'kernel': 'lv_kernel<10>', 'kernel_avg_us': round(kern_s * 1e6, 1),
                          'note': 'one thread per point running a divergent adaptive integration (~32 accepted '
                                  'steps + 2400 dense-output evaluations); 358 VGPRs -> one wave per SIMD; '
                                  '113 143 points fill 1 768 waves = 1.7 waves per SIMD'},
