@@ -40,6 +40,7 @@ for _p in (ROOT, PKG_ROOT):
 with open(os.path.join(ROOT, 'BASELINE.json')) as _f:
     BASELINE = json.load(_f)
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
+LV_FLOP_PER_OBS = 106   # dense output per observation: 10 x quartic (8) + x (2) + residual (2) + C^-1 (6) + 4 x 4
 FP64_VALU_PEAK_TFS = 78.6  # MI355X spec fp64 vector (256 CU x 4 SIMD x 16 FMA lanes x 2 x 2.4 GHz)
 
 LV_MEAN = np.array([-0.38261842, 0.29176476, -0.02010969, -0.01824518])
@@ -285,6 +286,7 @@ def main():
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
+    ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
     ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
     ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
@@ -829,8 +831,17 @@ def main_lv(args):
     out = torch.empty((m, 4), dtype=torch.float64, device=dev)
     status = torch.zeros(m, dtype=torch.int32, device=dev)
     L = nat.lib()
+    two_phase = args.lv_mode == 0
+    wb = int(L.st_lv_grad_workspace_bytes(m, t.size))
+    work = torch.empty((wb + 7) // 8, dtype=torch.float64, device=dev) if two_phase else None
 
     def run_once():
+        if two_phase:
+            nat.check(L.st_lv_grad_log_posterior_ws(nat.ptr(thd), m, nat.ptr(td), t.size, nat.ptr(yd), s.ctypes.data,
+                                                    cinv.ctypes.data, lv.MAX_STEPS, nat.ptr(out), nat.ptr(status),
+                                                    nat.ptr(work), wb, nat.stream_handle()),
+                      'st_lv_grad_log_posterior_ws')
+            return
         nat.check(L.st_lv_grad_log_posterior(nat.ptr(thd), m, nat.ptr(td), t.size, nat.ptr(yd), s.ctypes.data,
                                              cinv.ctypes.data, lv.MAX_STEPS, nat.ptr(out), nat.ptr(status),
                                              nat.stream_handle()), 'st_lv_grad_log_posterior')
@@ -851,6 +862,7 @@ def main_lv(args):
     elapsed = time.perf_counter() - t0
     kern_s = float(np.mean([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
     failed = int((status != 0).sum().item())
+    lv_flops = float(m) * t.size * LV_FLOP_PER_OBS
     if world > 1:
         dist.barrier()
         elapsed, kern_s = _max_over_ranks([elapsed, kern_s], dev)
@@ -864,11 +876,21 @@ def main_lv(args):
             'config': {'workload': 'LV gradients at 113 143 points (Dask_AWS unique-sample count), t_n = 2400, '
                                    'rtol 1e-3 / atol 1e-6', 'n': n,
                        'parallelism': f'point blocks x{world}' if world > 1 else 'single-gpu'},
-            'roofline': {'bound': 'latency', 'achieved': None, 'peak': None, 'unit': None, 'frac': None,
-                         'traffic': pmc_traffic('lv') if world == 1 else None, 'kernel': 'lv_kernel<10>', 'kernel_avg_us': round(kern_s * 1e6, 1),
-                         'note': 'one thread per point running a divergent adaptive integration (~32 accepted '
-                                 'steps + 2400 dense-output evaluations); 358 VGPRs -> one wave per SIMD; '
-                                 '113 143 points fill 1 768 waves = 1.7 waves per SIMD'},
+            'roofline': ({'bound': 'valu', 'achieved': round(lv_flops / kern_s / 1e12, 2), 'peak': FP64_VALU_PEAK_TFS,
+                          'unit': 'TFLOP/s', 'frac': round(lv_flops / kern_s / 1e12 / FP64_VALU_PEAK_TFS, 4),
+                          'traffic': pmc_traffic('lv2') if world == 1 else None,
+                          'kernel': 'lv_kernel<10,record> + lv_dense_kernel (+ overflow pass)',
+                          'kernel_avg_us': round(kern_s * 1e6, 1), 'flop_per_observation': LV_FLOP_PER_OBS,
+                          'note': 'priced on the dense-output work only (n x t_n observation points x '
+                                  f'{LV_FLOP_PER_OBS} flop: the quartic for 10 states, residual, C^-1 and the '
+                                  'sensitivity products); the RK45 integration (~32 accepted steps per point, '
+                                  'one thread each) is the serial part'} if two_phase else
+                         {'bound': 'latency', 'achieved': None, 'peak': None, 'unit': None, 'frac': None,
+                          'traffic': pmc_traffic('lv') if world == 1 else None, 'kernel': 'lv_kernel<10>',
+                          'kernel_avg_us': round(kern_s * 1e6, 1),
+                          'note': 'single-phase: one thread per point integrates and evaluates its 2400 '
+                                  'observation points; 354 VGPRs -> one wave per SIMD; 113 143 points fill 1 768 '
+                                  'waves = 1.7 waves per SIMD'}),
             'failed_points': failed,
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -389,6 +389,10 @@ int st_proxy_logpdf_grad(const double* x, int64_t n, int32_t d, const double* lo
     return hip_check(st::launch_proxy(a, static_cast<hipStream_t>(stream)), "proxy launch");
 }
 
+// accepted RK45 steps recorded per point by the two-phase gradient (typical: ~32 at the reference's
+// tolerances); a point that takes more is recomputed by the single-phase kernel
+constexpr int kLvStepCap = 64;
+
 static int lv_common(st::LvArgs& a, const double* theta, int64_t n, const double* t_eval, int32_t t_n,
                      const double* y_obs, const double* span_u0_tol, int64_t max_steps, double* out,
                      int32_t* status) {
@@ -425,6 +429,29 @@ int st_lv_grad_log_posterior(const double* theta, int64_t n, const double* t_eva
     if (rc) return rc;
     if (!cov_inv) return fail(ST_ERR_INVALID, "NULL cov_inv");
     for (int q = 0; q < 4; ++q) a.cinv[q] = cov_inv[q];
+    if (n == 0) return ST_OK;
+    return hip_check(st::launch_lv(a, true, static_cast<hipStream_t>(stream)), "lv gradient launch");
+}
+
+int64_t st_lv_grad_workspace_bytes(int64_t n, int32_t t_n) {
+    if (n < 0 || t_n < 1) return -1;
+    return st::lv_grad_workspace_bytes(n, kLvStepCap);
+}
+
+int st_lv_grad_log_posterior_ws(const double* theta, int64_t n, const double* t_eval, int32_t t_n,
+                                const double* y_obs, const double* span_u0_tol, const double* cov_inv,
+                                int64_t max_steps, double* grad_out, int32_t* status, void* workspace,
+                                int64_t workspace_bytes, void* stream) {
+    st::LvArgs a{};
+    int rc = lv_common(a, theta, n, t_eval, t_n, y_obs, span_u0_tol, max_steps, grad_out, status);
+    if (rc) return rc;
+    if (!cov_inv) return fail(ST_ERR_INVALID, "NULL cov_inv");
+    if (n > 0 && !workspace) return fail(ST_ERR_INVALID, "NULL workspace");
+    if (workspace_bytes < st::lv_grad_workspace_bytes(n, kLvStepCap)) return fail(ST_ERR_INVALID, "workspace too small");
+    for (int q = 0; q < 4; ++q) a.cinv[q] = cov_inv[q];
+    a.step_cap = kLvStepCap;
+    a.steps = static_cast<double*>(workspace);
+    a.nsteps = reinterpret_cast<int32_t*>(static_cast<char*>(workspace) + n * (int64_t)kLvStepCap * 56 * 8);
     if (n == 0) return ST_OK;
     return hip_check(st::launch_lv(a, true, static_cast<hipStream_t>(stream)), "lv gradient launch");
 }

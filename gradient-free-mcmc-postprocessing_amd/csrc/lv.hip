@@ -25,6 +25,8 @@ namespace st {
 namespace {
 
 constexpr int kLvThreads = 64;
+constexpr int kLvOverflow = 3;     // status: more accepted steps than the step table holds (internal)
+constexpr int kLvStepRec = 56;     // doubles per recorded step: t_old, 1/h, k_begin, k_end, y[10], hQ[10][4], pad
 
 template <int NS>
 __device__ inline void lv_rhs(const double th[4], const double* y, double* f) {
@@ -56,11 +58,19 @@ __device__ inline double rms(const double* v) {
 }
 
 // NS = 10: gradient of the log posterior -> out[4 i + j]; NS = 2: per-time log-likelihood terms ->
-// work[k n + i] (summed by lv_logdens_finish)
-template <int NS>
+// work[k n + i] (summed by lv_logdens_finish).
+// RECORD (NS = 10, two-phase gradient): instead of evaluating the observation points while it
+// integrates, the thread stores every accepted step's dense-output polynomial (t_old, 1/h, the
+// observation range, y_old, hQ) in the step table a.steps[i][s] and leaves the points to
+// lv_dense_kernel (one wave per parameter point); a point with more than a.step_cap accepted
+// steps gets status kLvOverflow and is recomputed by the single-phase kernel (ONLY_OVERFLOW).
+template <int NS, bool RECORD = false, bool ONLY_OVERFLOW = false>
 __global__ __launch_bounds__(kLvThreads) void lv_kernel(LvArgs a) {
     const int64_t i = (int64_t)blockIdx.x * kLvThreads + threadIdx.x;
     if (i >= a.n) return;
+    if constexpr (ONLY_OVERFLOW) {
+        if (a.status[i] != kLvOverflow) return;
+    }
     double th[4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) th[j] = a.theta[4 * i + j];
@@ -99,6 +109,7 @@ __global__ __launch_bounds__(kLvThreads) void lv_kernel(LvArgs a) {
         h_abs = fmin(fmin(100 * h0, h1), interval);   // max_step = inf
     }
     int kk = 0;                       // next observation point
+    int nrec = 0;                     // RECORD: accepted steps stored
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
     int32_t status = 0;
     for (int64_t step = 0;; ++step) {
@@ -182,7 +193,35 @@ __global__ __launch_bounds__(kLvThreads) void lv_kernel(LvArgs a) {
             }
         static_assert(rk45::kDenseOrder == 4, "Horner form below is written for RK45's quartic");
         const bool last = t_new - t_bound >= 0;
-        while (kk < a.t_n && (last || a.t_eval[kk] <= t_new)) {
+        if constexpr (RECORD) {
+            // observation range of this step: (t_old, t_new], everything left at the last step
+            int k_end = a.t_n;
+            if (!last) {
+                int lo = kk, hi = a.t_n;   // first index with t_eval > t_new
+                while (lo < hi) {
+                    const int mid = (lo + hi) >> 1;
+                    if (a.t_eval[mid] <= t_new) lo = mid + 1; else hi = mid;
+                }
+                k_end = lo;
+            }
+            if (k_end > kk) {
+                if (nrec >= a.step_cap) { status = kLvOverflow; break; }
+                double* r = a.steps + ((int64_t)i * a.step_cap + nrec) * kLvStepRec;
+                r[0] = t_old;
+                r[1] = inv_hd;
+                r[2] = (double)kk;
+                r[3] = (double)k_end;
+#pragma unroll
+                for (int c = 0; c < NS; ++c) {
+                    r[4 + c] = y[c];
+#pragma unroll
+                    for (int q = 0; q < rk45::kDenseOrder; ++q) r[4 + NS + 4 * c + q] = Q[c][q];
+                }
+                ++nrec;
+                kk = k_end;
+            }
+        }
+        while (!RECORD && kk < a.t_n && (last || a.t_eval[kk] <= t_new)) {
             const double x = (a.t_eval[kk] - t_old) * inv_hd;
             double u[NS];
 #pragma unroll
@@ -207,6 +246,15 @@ __global__ __launch_bounds__(kLvThreads) void lv_kernel(LvArgs a) {
         for (int c = 0; c < NS; ++c) { y[c] = y_new[c]; f[c] = f_new[c]; }
     }
     a.status[i] = status;
+    if constexpr (RECORD) {
+        a.nsteps[i] = nrec;
+        if (status == kLvOverflow) return;
+        if (status) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) a.out[4 * i + j] = NAN;
+        }
+        return;
+    }
     if constexpr (NS == 10) {
 #pragma unroll
         for (int j = 0; j < 4; ++j)
@@ -284,11 +332,130 @@ __global__ __launch_bounds__(kLvThreads) void lv_logdens_finish(LvArgs a) {
     a.out[i] = ll + lp;
 }
 
+__device__ __forceinline__ int wave_sum_int(int v) {
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// Phase B of the two-phase gradient: one wave per parameter point.  Each recorded step's
+// observation range is cut into pieces of at most P points, P the smallest piece length that
+// yields at most 64 pieces (one per lane, one round); lane L takes piece L, loads its step record
+// once (y_old, hQ, t_old, 1/h: no search or reload inside a piece) and accumulates
+// J^T C^-1 (y_k - u(t_k)) over the piece in its own partial sums; the wave then adds the 64 partial
+// sums.  The per-point sum is thus reassociated (pieces, then a tree) against the reference's
+// sequential np.sum -- within the same 1e-8 tolerance as the BLAS-ordered stages
+// (tests/test_gpu_lv.py).
+__global__ __launch_bounds__(256) void lv_dense_kernel(LvArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    __shared__ int pstart_sh[4][65];
+    if (i >= a.n) return;                   // (wave-uniform: the whole wave leaves)
+    if (a.status[i] != 0) return;          // NaN already written, or the overflow kernel's point
+    const int ns = a.nsteps[i];            // <= step_cap <= 64
+    const double* tab = a.steps + (int64_t)i * a.step_cap * kLvStepRec;
+    int* pstart = pstart_sh[threadIdx.x >> 6];
+    int kb_s = 0, len = 0;                  // step `lane`: first observation, count
+    if (lane < ns) {
+        const double* r = tab + (int64_t)lane * kLvStepRec;
+        kb_s = (int)r[2];
+        len = (int)r[3] - kb_s;
+    }
+    // smallest P with sum_s ceil(len_s / P) <= 64 (ns <= 64 guarantees P = max len qualifies)
+    int plo = (a.t_n + 63) / 64, phi = len;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) phi = max(phi, __shfl_xor(phi, off));
+    if (plo > phi) plo = phi;
+    while (plo < phi) {
+        const int mid = (plo + phi) >> 1;
+        if (wave_sum_int((len + mid - 1) / mid) <= 64) phi = mid; else plo = mid + 1;
+    }
+    const int P = plo > 0 ? plo : 1;
+    const int np = (len + P - 1) / P;
+    int incl = np;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int o = __shfl_up(incl, off);
+        if (lane >= off) incl += o;
+    }
+    pstart[lane + 1] = incl;
+    if (lane == 0) pstart[0] = 0;
+    __builtin_amdgcn_wave_barrier();
+    const int total = __shfl(incl, 63);   // <= 64
+    double acc[4] = {0.0, 0.0, 0.0, 0.0};
+    if (lane < total) {
+        int lo = 0, hi = ns - 1;           // step s with pstart[s] <= lane < pstart[s + 1]
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (pstart[mid] <= lane) lo = mid; else hi = mid - 1;
+        }
+        const double* r = tab + (int64_t)lo * kLvStepRec;
+        const double2* r2 = reinterpret_cast<const double2*>(r);
+        const double2 h0 = r2[0], h1 = r2[1];
+        const double t_old = h0.x, inv_hd = h0.y;
+        const int kb = (int)h1.x + (lane - pstart[lo]) * P;
+        const int ke = kb + P < (int)h1.y ? kb + P : (int)h1.y;
+        double y[10], Q[10][4];
+#pragma unroll
+        for (int c = 0; c < 10; c += 2) {
+            const double2 v = r2[2 + c / 2];
+            y[c] = v.x;
+            y[c + 1] = v.y;
+        }
+#pragma unroll
+        for (int c = 0; c < 10; ++c) {
+            const double2 v0 = r2[7 + 2 * c], v1 = r2[8 + 2 * c];
+            Q[c][0] = v0.x; Q[c][1] = v0.y; Q[c][2] = v1.x; Q[c][3] = v1.y;
+        }
+        for (int k = kb; k < ke; ++k) {
+            const double x = (a.t_eval[k] - t_old) * inv_hd;
+            double u[10];
+#pragma unroll
+            for (int c = 0; c < 10; ++c)
+                u[c] = __builtin_fma(x, __builtin_fma(x, __builtin_fma(x, __builtin_fma(x, Q[c][3], Q[c][2]),
+                                                                       Q[c][1]), Q[c][0]), y[c]);
+            const double r0 = a.y_obs[2 * k] - u[0], r1 = a.y_obs[2 * k + 1] - u[1];
+            const double g0 = a.cinv[0] * r0 + a.cinv[1] * r1;
+            const double g1 = a.cinv[2] * r0 + a.cinv[3] * r1;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) acc[j] += u[2 + j] * g0 + u[6 + j] * g1;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        double v = acc[j];
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) v += __shfl_xor(v, off);
+        acc[j] = v;
+    }
+    if (lane == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const double th = a.theta[4 * i + j];
+            a.out[4 * i + j] = acc[j] - log(th) / th;
+        }
+    }
+}
+
 }  // namespace
+
+int64_t lv_grad_workspace_bytes(int64_t n, int step_cap) {
+    return n * ((int64_t)step_cap * kLvStepRec * 8 + 8);
+}
 
 hipError_t launch_lv(const LvArgs& a, bool gradient, hipStream_t s) {
     if (a.n <= 0) return hipSuccess;
     const unsigned blocks = (unsigned)((a.n + kLvThreads - 1) / kLvThreads);
+    if (gradient && a.steps) {   // two-phase: record, dense per wave, overflowed points single-phase
+        if (a.step_cap < 1 || a.step_cap > 64) return hipErrorInvalidValue;   // one step per lane in lv_dense_kernel
+        lv_kernel<10, true><<<blocks, kLvThreads, 0, s>>>(a);
+        hipError_t e = hipGetLastError();
+        if (e != hipSuccess) return e;
+        lv_dense_kernel<<<(unsigned)((a.n + 3) / 4), 256, 0, s>>>(a);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+        lv_kernel<10, false, true><<<blocks, kLvThreads, 0, s>>>(a);
+        return hipGetLastError();
+    }
     if (gradient) {
         lv_kernel<10><<<blocks, kLvThreads, 0, s>>>(a);
         return hipGetLastError();

@@ -112,8 +112,12 @@ struct LvArgs {
     double* out;              // gradient: (n, 4); log density: (n)
     double* work;             // log density: (t_n, n) per-time terms
     int32_t* status;          // (n): 0 ok, 1 step size too small, 2 step limit reached
+    double* steps;            // gradient, two-phase: (n, step_cap, 56) step table, or nullptr
+    int32_t* nsteps;          // (n) recorded steps per point
+    int step_cap;
 };
 hipError_t launch_lv(const LvArgs& a, bool gradient, hipStream_t s);
+int64_t lv_grad_workspace_bytes(int64_t n, int step_cap);
 
 hipError_t launch_greedy_rank_exchange(const double* recs, int K, int64_t stride, int d,
                                        const MailboxPeers& peers, int rank, int nranks, int64_t t,

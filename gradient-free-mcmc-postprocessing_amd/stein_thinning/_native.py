@@ -79,6 +79,9 @@ SIGNATURES = {
                                                _c_dp, _i64, _c_dp, _c_dp]),
     'st_lv_grad_log_posterior': (ctypes.c_int, [_c_dp, _i64, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _i64, _c_dp,
                                                 _c_dp, _c_dp]),
+    'st_lv_grad_workspace_bytes': (_i64, [_i64, _i32]),
+    'st_lv_grad_log_posterior_ws': (ctypes.c_int, [_c_dp, _i64, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _i64, _c_dp,
+                                                   _c_dp, _c_dp, _i64, _c_dp]),
     'st_lv_log_density_workspace_bytes': (_i64, [_i64, _i32]),
     'st_lv_log_target_density': (ctypes.c_int, [_c_dp, _c_dp, _i64, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _f64,
                                                 _f64, _i64, _c_dp, _c_dp, _c_dp, _i64, _c_dp]),

@@ -90,9 +90,10 @@ def _status_check(status: np.ndarray, what: str):
 
 
 def grad_log_posterior(theta, data: Optional[LvData] = None, rtol: float = RTOL, atol: float = ATOL,
-                       max_steps: int = MAX_STEPS) -> np.ndarray:
+                       max_steps: int = MAX_STEPS, chunk: int = 1 << 16) -> np.ndarray:
     """``grad_log_posterior`` of Sensitivity_analysis.ipynb cell 46 for every row of ``theta``
-    ((n, 4) or (4,)): returns (n, 4)."""
+    ((n, 4) or (4,)): returns (n, 4).  Two-phase kernels (``st_lv_grad_log_posterior_ws``), at most
+    ``chunk`` points per launch (the step table is ~29 KB per point)."""
     import torch
     data = reference_data() if data is None else data
     th = _points(theta)
@@ -103,10 +104,17 @@ def grad_log_posterior(theta, data: Optional[LvData] = None, rtol: float = RTOL,
     out = torch.empty((max(n, 1), 4), dtype=torch.float64, device=dev)
     status = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
     if n:
+        L = nat.lib()
         thd, td, yd = (torch.from_numpy(a).to(dev) for a in (th, t, y))
-        nat.check(nat.lib().st_lv_grad_log_posterior(
-            nat.ptr(thd), n, nat.ptr(td), t.size, nat.ptr(yd), s.ctypes.data, cinv.ctypes.data, int(max_steps),
-            nat.ptr(out), nat.ptr(status), nat.stream_handle()), 'st_lv_grad_log_posterior')
+        m = min(n, chunk)
+        wb = int(L.st_lv_grad_workspace_bytes(m, t.size))
+        work = torch.empty((wb + 7) // 8, dtype=torch.float64, device=dev)
+        for c0 in range(0, n, chunk):
+            c1 = min(n, c0 + chunk)
+            nat.check(L.st_lv_grad_log_posterior_ws(
+                nat.ptr(thd[c0:c1]), c1 - c0, nat.ptr(td), t.size, nat.ptr(yd), s.ctypes.data, cinv.ctypes.data,
+                int(max_steps), nat.ptr(out[c0:c1]), nat.ptr(status[c0:c1]), nat.ptr(work), wb,
+                nat.stream_handle()), 'st_lv_grad_log_posterior_ws')
     res, st = out[:n].cpu().numpy(), status[:n].cpu().numpy()
     _status_check(st, 'grad_log_posterior')
     return res

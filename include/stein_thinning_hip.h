@@ -222,6 +222,15 @@ int st_kde_logpdf_grad(const double *p_soa, int64_t ldp, int64_t n, const double
 int st_lv_grad_log_posterior(const double *theta, int64_t n, const double *t_eval, int32_t t_n,
                              const double *y_obs, const double *span_u0_tol, const double *cov_inv,
                              int64_t max_steps, double *grad_out, int32_t *status, void *stream);
+/* Two-phase form of st_lv_grad_log_posterior (same arguments and results, faster): the integration
+ * records each accepted step's dense-output polynomial in the workspace and the observation points
+ * are evaluated one wave per parameter point; workspace: st_lv_grad_workspace_bytes(n, t_n) bytes
+ * of device memory. */
+int64_t st_lv_grad_workspace_bytes(int64_t n, int32_t t_n);
+int st_lv_grad_log_posterior_ws(const double *theta, int64_t n, const double *t_eval, int32_t t_n,
+                                const double *y_obs, const double *span_u0_tol, const double *cov_inv,
+                                int64_t max_steps, double *grad_out, int32_t *status, void *workspace,
+                                int64_t workspace_bytes, void *stream);
 int64_t st_lv_log_density_workspace_bytes(int64_t n, int32_t t_n);
 int st_lv_log_target_density(const double *log_theta, const double *theta, int64_t n,
                              const double *t_eval, int32_t t_n, const double *y_obs,

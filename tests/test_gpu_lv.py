@@ -81,3 +81,46 @@ def test_single_point_and_empty(data):
     assert g1.shape == (1, 4)
     assert lv.grad_log_posterior(np.zeros((0, 4)), data).shape == (0, 4)
     assert lv.log_target_density(np.zeros((0, 4)), data).shape == (0,)
+
+
+def _single_phase(th, data, rtol=lv.RTOL, atol=lv.ATOL):
+    """st_lv_grad_log_posterior: the one-kernel path (each thread integrates and evaluates)."""
+    from stein_thinning import _native as nat
+    th = np.ascontiguousarray(th, dtype=np.float64)
+    t, y, s = lv._settings(data, rtol, atol)
+    cinv = np.ascontiguousarray(np.linalg.inv(np.asarray(data.cov, dtype=np.float64)))
+    dev = nat.require_device()
+    n = th.shape[0]
+    out = torch.empty((n, 4), dtype=torch.float64, device=dev)
+    status = torch.zeros(n, dtype=torch.int32, device=dev)
+    thd, td, yd = (torch.from_numpy(a).to(dev) for a in (th, t, y))
+    nat.check(nat.lib().st_lv_grad_log_posterior(
+        nat.ptr(thd), n, nat.ptr(td), t.size, nat.ptr(yd), s.ctypes.data, cinv.ctypes.data, lv.MAX_STEPS,
+        nat.ptr(out), nat.ptr(status), nat.stream_handle()), 'st_lv_grad_log_posterior')
+    assert int((status != 0).sum()) == 0
+    return out.cpu().numpy()
+
+
+def test_two_phase_matches_single_phase(data):
+    """The two-phase gradient (recorded steps, one wave per point) reassociates only the dense
+    output and the sum over observation points: same step sequence, values to ~1e-13."""
+    th = _thetas()
+    got = lv.grad_log_posterior(th, data)
+    want = _single_phase(th, data)
+    err = np.abs(got - want) / np.abs(want).max(axis=1, keepdims=True)
+    print('max rel diff', err.max())
+    assert err.max() < 1e-11
+
+
+def test_two_phase_step_table_overflow_falls_back(data):
+    """rtol 1e-9 needs far more than the 64 recorded steps per point: every point overflows the
+    step table and is recomputed by the single-phase kernel -- bitwise its result."""
+    th = _points(70, 0.05, 6)
+    got = lv.grad_log_posterior(th, data, rtol=1e-9, atol=1e-12)
+    want = _single_phase(th, data, rtol=1e-9, atol=1e-12)
+    np.testing.assert_array_equal(got, want)
+
+
+def test_two_phase_chunks(data):
+    th = _points(50, 0.05, 7)
+    np.testing.assert_array_equal(lv.grad_log_posterior(th, data, chunk=7), lv.grad_log_posterior(th, data))
