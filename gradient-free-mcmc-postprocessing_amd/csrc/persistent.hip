@@ -168,6 +168,9 @@ struct PersistArgs {
     uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
     int rec_stride;               // record pitch in granules (2 = packed; wider spreads the polled
                                   // records over more memory channels)
+    int nrep;                     // record replicas: every block stores its record into each of
+                                  // them, block b sweeps replica b % nrep (fewer readers per line)
+    int64_t rep_stride;           // granules between replicas (and between banks' replica sets)
     int64_t row_begin, row_end;   // this rank's rows (global indices); one device: [0, n)
     int rank, nranks;
     uint64_t seq_base;            // exchange sequence number of step 0 (mailbox banks / tags)
@@ -207,6 +210,11 @@ constexpr int kRecGranules = 2;
 // bytes between consecutive blocks' records: 256 spreads the 256 polled records of a step over
 // more memory channels than 16-B packing (-0.3 us per step, profiles/r01_sweep_pitch.log)
 constexpr int kDefaultRecPitch = 256;
+// replicas of the record array (st_tune key 10): every block stores its record into each replica
+// (16-B sc1 stores by 16 lanes) and block b sweeps replica b % 16, densely packed: 16 readers per
+// line instead of 256, 32 lines per poll instead of 256.  Config 4: 11.6 -> 11.1 ms per thin;
+// n = 2.5e5 per device (one rank of 8): 4.80 -> 4.47 us per step (profiles/r02_record_replicas.log)
+constexpr int kDefaultRecReplicas = 16;
 constexpr int64_t kNt512MinRows = 1280;
 
 __device__ __forceinline__ uint64_t step_tag(int64_t t) { return (uint64_t)((t + 1) & 0xFF) << 56; }
@@ -221,19 +229,43 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) { sc->v[wave] = v; sc->i[wave] = li; }
     __syncthreads();
-    if (threadIdx.x == 0) {   // ONE lane combines the wave minima and stores the two granules
+    if (a.nrep == 1) {
+        if (threadIdx.x == 0) {   // ONE lane combines the wave minima and stores the two granules
+            v = sc->v[0];
+            li = sc->i[0];
+#pragma unroll
+            for (int w = 1; w < NT / 64; ++w) take_if_better(sc->v[w], sc->i[w], v, li);
+            sc->vblk = v;   // read by every thread after wait_and_pick's barrier
+            uint64_t* gr = a.gran + (t & 1) * a.rep_stride + (int64_t)blockIdx.x * a.rec_stride;
+            const uint64_t tag = step_tag(t);
+            const uint64_t vb = (uint64_t)__double_as_longlong(v);
+            const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
+            __hip_atomic_store(gr + 0, tag | (vb >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gr + 1, tag | ((vb & 0xFFull) << 32) | ib, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        }
+    } else if (threadIdx.x < 64) {
+        // replicated records: wave 0 combines (every lane the same values from LDS) and lane r
+        // stores the record into replica r as ONE 16-B sc1 store (both granules tagged: a torn
+        // store fails the reader's tag check like two 8-B stores would)
         v = sc->v[0];
         li = sc->i[0];
 #pragma unroll
         for (int w = 1; w < NT / 64; ++w) take_if_better(sc->v[w], sc->i[w], v, li);
-        sc->vblk = v;   // read by every thread after wait_and_pick's barrier
-        uint64_t* gr = a.gran + ((t & 1) * (int64_t)gridDim.x + blockIdx.x) * a.rec_stride;
-        const uint64_t tag = step_tag(t);
-        const uint64_t vb = (uint64_t)__double_as_longlong(v);
-        const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
-        __hip_atomic_store(gr + 0, tag | (vb >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(gr + 1, tag | ((vb & 0xFFull) << 32) | ib, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
+        if (threadIdx.x == 0) sc->vblk = v;
+        if ((int)threadIdx.x < a.nrep) {
+            const uint64_t tag = step_tag(t);
+            const uint64_t vb = (uint64_t)__double_as_longlong(v);
+            const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
+            const uint64_t g0 = tag | (vb >> 8), g1 = tag | ((vb & 0xFFull) << 32) | ib;
+            const int64_t off = (((t & 1) * a.nrep + threadIdx.x) * a.rep_stride +
+                                 (int64_t)blockIdx.x * a.rec_stride) * 8;
+            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.gran, 0, 0x7FFFFFFF, 0x00020000);
+            typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+            __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)g0, (unsigned)(g0 >> 32), (unsigned)g1,
+                                                         (unsigned)(g1 >> 32)},
+                                                   rsrc, (int)off, 0, 16 /* sc1 */);
+        }
     }
 }
 
@@ -256,7 +288,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
     ST_STAMP(a, t + 1, 0);
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const uint64_t* bank = a.gran + (t & 1) * (int64_t)G * a.rec_stride;
+        const uint64_t* bank = a.gran + ((t & 1) * a.nrep + (int)blockIdx.x % a.nrep) * a.rep_stride;
         const uint64_t want = step_tag(t);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         uint32_t need = 0;
@@ -282,24 +314,25 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             }
         };
         int ok_all = 1;
-        unsigned it = 0;
+        unsigned it = 0;   // polls taken
         // one 16-B sc1 buffer load per record (both granules; a torn pair fails its tag check)
         const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<uint64_t*>(bank), 0,
                                                             G * a.rec_stride * 8, 0x00020000);
         typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-        for (;; ++it) {
-            // all four loads unconditionally (records past G read as zeros: the descriptor's range
-            // check), so they issue back to back and a poll costs ONE round trip, not four; a record
-            // already seen is re-read at an out-of-range offset (zeros, no memory access), so later
-            // polls only load what is still missing
-            u32x4 qs[MAXG / 64];
-            const uint32_t oob = (uint32_t)G * a.rec_stride * 8;
+        // all four loads unconditionally (records past G read as zeros: the descriptor's range
+        // check), so they issue back to back and a poll costs ONE round trip, not four; a record
+        // already seen is re-read at an out-of-range offset (zeros, no memory access), so later
+        // polls only load what is still missing
+        const uint32_t oob = (uint32_t)G * a.rec_stride * 8;
+        auto issue = [&](u32x4 (&qs)[MAXG / 64]) {
 #pragma unroll
             for (int c = 0; c < MAXG / 64; ++c) {
                 const uint32_t off = (uint32_t)(lane + 64 * c) * a.rec_stride * 8;
                 qs[c] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((need & ~seen) >> c) & 1u ? off : oob,
                                                               0, 16 /* sc1 */);
             }
+        };
+        auto take = [&](const u32x4 (&qs)[MAXG / 64]) {
 #pragma unroll
             for (int c = 0; c < MAXG / 64; ++c) {
                 if ((need & ~seen) & (1u << c)) {
@@ -316,18 +349,31 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                     }
                 }
             }
-            if (__all(seen == need)) break;
-            if (gi != row_of && gi != INT64_MAX) {   // speculative row of the best so far
+        };
+        // after a poll: speculative row of the best so far; every 16 polls the bounded-wait check
+        auto between = [&]() -> bool {
+            if (gi != row_of && gi != INT64_MAX) {
                 load_row(gi);
                 row_of = gi;
             }
-            __builtin_amdgcn_s_sleep(1);
             if ((it & 15) == 15) {
                 const bool late = __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks;
                 const bool other = __hip_atomic_load(a.status, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT) != 0;
-                if (__any(late || other)) { ok_all = 0; break; }
+                if (__any(late || other)) { ok_all = 0; return false; }
             }
+            ++it;
+            return true;
+        };
+        // one poll in flight (two staggered polls were measured slower at every stagger, with
+        // and without replicas: profiles/r02_poll_stagger_rejected.log)
+        for (;;) {
+            u32x4 qs[MAXG / 64];
+            issue(qs);
+            take(qs);
+            if (__all(seen == need)) break;
+            if (!between()) break;
+            __builtin_amdgcn_s_sleep(1);
         }
         ST_STAMP(a, t + 1, 1);
 #ifdef ST_PERSIST_STAMPS
@@ -805,10 +851,17 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
-int64_t persistent_ws_bytes(int d, int G, int rec_stride) {
-    // [control: status (and reserved) words][2 banks x G records, rec_stride granules of 8 B apart]
+// granules between replicas: one replica = G records rec_stride granules apart; with several
+// replicas each starts on a fresh 512-B boundary plus 256 B, so their lines fall on other channels
+int64_t persistent_rep_stride(int G, int rec_stride, int nrep) {
+    const int64_t one = (int64_t)G * rec_stride;
+    return nrep == 1 ? one : (one + 63) / 64 * 64 + 32;
+}
+
+int64_t persistent_ws_bytes(int d, int G, int rec_stride, int nrep) {
+    // [control: status (and reserved) words][2 banks x nrep replicas x G records]
     (void)d;
-    return kWsControlBytes + 2 * (int64_t)G * rec_stride * 8;
+    return kWsControlBytes + 2 * (int64_t)nrep * persistent_rep_stride(G, rec_stride, nrep) * 8;
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
@@ -816,6 +869,7 @@ static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (25
 static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (one per CU)
 static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
 static int g_persist_pitch = -1; // st_tune key 9: record pitch in bytes (16 .. 4096, power of 2), -1 auto
+static int g_persist_nrep = -1;  // st_tune key 10: record replicas (1 .. 32, power of 2), -1 auto
 static uint64_t* g_stamps = nullptr;
 #ifdef ST_PERSIST_STAMPS
 extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
@@ -844,6 +898,11 @@ int persistent_tune(int key, int value) {
     if (key == 9) {
         if (value != -1 && (value < 16 || value > 4096 || (value & (value - 1)))) return -1;
         g_persist_pitch = value;
+        return 0;
+    }
+    if (key == 10) {
+        if (value != -1 && (value < 1 || value > 32 || (value & (value - 1)))) return -1;
+        g_persist_nrep = value;
         return 0;
     }
     return -1;
@@ -935,9 +994,13 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     if (n_shard < (int64_t)G * min_rows) G = (int)((n_shard + min_rows - 1) / min_rows);
     if (G < 1) G = 1;
     // record pitch: the widest requested / default that the workspace holds (>= 16 B)
-    int pitch = (g_persist_pitch > 0 ? g_persist_pitch : kDefaultRecPitch) / 8;
-    while (pitch > kRecGranules && persistent_ws_bytes(d, G, pitch) > ws_bytes) pitch /= 2;
-    if (persistent_ws_bytes(d, G, pitch) > ws_bytes) return hipErrorNotSupported;
+    int nrep = g_persist_nrep > 0 ? g_persist_nrep : kDefaultRecReplicas;
+    if (nrep > G) nrep = G;
+    while (nrep & (nrep - 1)) nrep &= nrep - 1;
+    int pitch = (g_persist_pitch > 0 ? g_persist_pitch : (nrep > 1 ? 16 : kDefaultRecPitch)) / 8;
+    while (nrep > 1 && persistent_ws_bytes(d, G, pitch, nrep) > ws_bytes) nrep /= 2;
+    while (pitch > kRecGranules && persistent_ws_bytes(d, G, pitch, nrep) > ws_bytes) pitch /= 2;
+    if (persistent_ws_bytes(d, G, pitch, nrep) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n_shard + G - 1) / G;
     if (wide && R > 256) return hipErrorNotSupported;   // wide: one register row per thread only
     // auto: 512-thread blocks (two waves per SIMD, dynamic chunks) once a block has more rows than
@@ -980,6 +1043,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.rows_per_block = R;
     a.RL = (int)RL;
     a.rec_stride = pitch;
+    a.nrep = nrep;
+    a.rep_stride = persistent_rep_stride(G, pitch, nrep);
     a.stamps = g_stamps;
     a.row_begin = rs->row_begin;
     a.row_end = rs->row_end;
@@ -989,7 +1054,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.inbox = rs->inbox;
     for (int r = 0; r < kMaxRanks; ++r) a.peer[r] = r < rs->nranks ? rs->peer[r] : nullptr;
     // zero status and every granule tag (a stale tag from a previous run must never match)
-    hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G, pitch), s);
+    hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G, pitch, nrep), s);
     if (e != hipSuccess) return e;
     e = launch_kind(a, d, wide, gf, rt, nt, bpc, G, lds, s, false);
     if (e == hipSuccess) *used = 1;

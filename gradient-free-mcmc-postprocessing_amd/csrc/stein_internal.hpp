@@ -62,7 +62,7 @@ struct GreedyArgs {
 int greedy_blocks(int64_t n, int d);
 int tune(int key, int value);
 int persistent_tune(int key, int value);
-int64_t persistent_ws_bytes(int d, int G, int rec_stride);
+int64_t persistent_ws_bytes(int d, int G, int rec_stride, int nrep);
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,

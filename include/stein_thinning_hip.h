@@ -62,8 +62,10 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * 1..256; -1 = one per CU), key 6 = grid cap of the d > 8 step kernel (1..1024), key 7 = proxy
  * kernel (0 = automatic: matrix cores for 16 < d <= 64; 1 = always the VALU kernel), key 8 =
  * persistent kernel blocks per CU (1, 2; -1 = automatic = 1), key 9 = persistent kernel
- * record pitch in bytes (power of two, 16..4096; -1 = automatic = 256, narrowed to what the
- * workspace holds).
+ * record pitch in bytes (power of two, 16..4096; -1 = automatic = 256 with one replica, 16 with
+ * several, narrowed to what the workspace holds), key 10 = persistent kernel record replicas
+ * (power of two, 1..32: every block stores its per-step record into each replica and block b
+ * sweeps replica b % replicas; -1 = automatic).
  */
 int st_tune(int32_t key, int32_t value);
 

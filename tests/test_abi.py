@@ -109,3 +109,18 @@ def test_library_is_gfx950_only(libpath):
     blob = open(libpath, 'rb').read()
     targets = set(re.findall(rb'amdgcn-amd-amdhsa--(gfx[0-9a-z]+)', blob))
     assert targets == {b'gfx950'}, targets
+
+
+def test_tune_keys_validate_without_gpu(libpath):
+    """st_tune only records host-side knobs: valid values are accepted and restored, invalid ones
+    rejected (record replicas: powers of two 1..32; record pitch: powers of two 16..4096)."""
+    from stein_thinning import _native
+    lib = _native.load_library(libpath)
+    for key, good, bad in [(10, [1, 2, 16, 32], [0, 3, 64]), (9, [16, 256, 4096], [8, 24, 8192]),
+                           (4, [256, 512], [128, 1024]), (8, [1, 2], [3])]:
+        for v in good:
+            assert lib.st_tune(key, v) == 0, (key, v)
+        for v in bad:
+            assert lib.st_tune(key, v) != 0, (key, v)
+        assert lib.st_tune(key, -1) == 0
+    assert lib.st_tune(99, 1) != 0

@@ -182,11 +182,15 @@ def test_persistent_and_fallback_bit_exact(tune):
     ('512-thread blocks, 4 register rows', {4: 512, 3: 4}),
     ('256-thread blocks (one wave per SIMD), LDS and streamed rows', {4: 256}),
     ('512-thread blocks, packed 16-B records', {4: 512, 9: 16}),
+    ('one record array, 256-B pitch (no replicas)', {10: 1}),
+    ('4 record replicas', {10: 4}),
+    ('32 record replicas, 64-B pitch', {10: 32, 9: 64}),
+    ('two blocks per CU, 32 record replicas (512 records per step)', {8: 2, 10: 32}),
 ])
 @pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
 def test_persistent_two_wave_variants_bit_exact(knobs, d, gf):
-    """The optional two-waves-per-SIMD persistent variants (st_tune keys 3, 4, 8) against the C
-    model: identical indices, bit-identical running sums."""
+    """The optional two-waves-per-SIMD persistent variants (st_tune keys 3, 4, 8) and record
+    layouts (keys 9, 10) against the C model: identical indices, bit-identical running sums."""
     from stein_thinning import _native
     n, m = 700_001, 20
     x, g = _rw_chain(n, d, seed=11 + d)
@@ -203,7 +207,7 @@ def test_persistent_two_wave_variants_bit_exact(knobs, d, gf):
     try:
         idx, A = DeviceProblem(s, gs, w, l, tr).greedy(m, return_sums=True)
     finally:
-        for k in (3, 4, 8, 9):
+        for k in (3, 4, 8, 9, 10):
             L.st_tune(k, -1)
     cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
     np.testing.assert_array_equal(idx, cidx)

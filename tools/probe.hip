@@ -102,7 +102,7 @@ int main(int argc, char** argv) {
     const double bytes_rw = (double)n * (16 * d + 16), bytes_r = (double)n * (16 * d + 8);
     printf("# n=%lld d=%d  step traffic %.1f MB (read %.1f MB)\n", (long long)n, d, bytes_rw / 1e6, bytes_r / 1e6);
     const int reps = 200;
-    const bool persist_only = argc > 2 && argv[2][0] == 'p';
+    const bool persist_only = argc > 2 && (argv[2][0] == 'p' || argv[2][0] == 'r');
     for (int blocks : {256, 512, 1024, 2048, 4096}) {
         if (persist_only) break;
         for (int wr = 0; wr < 2; ++wr) {
@@ -163,6 +163,32 @@ int main(int argc, char** argv) {
         }
     }
     st_tune(0, 256); st_tune(1, -1); st_tune(2, -1);
+    if (argc > 2 && argv[2][0] == 'r') {   // record replicas (st_tune key 10) x pitch (key 9), m = 1000
+        const int Mr = 1000;
+        std::vector<uint32_t> ref;
+        struct RV { int nrep, pitch; };
+        for (int pass = 0; pass < 2; ++pass)
+        for (RV cfg : {RV{1, -1}, RV{2, 16}, RV{4, 16}, RV{8, 16}, RV{8, 64}, RV{16, 16},
+                       RV{32, 16}, RV{8, 256}}) {
+            if (st_tune(10, cfg.nrep) || st_tune(9, cfg.pitch)) { fprintf(stderr, "tune\n"); exit(1); }
+            std::vector<float> v;
+            std::vector<uint32_t> h(Mr);
+            for (int rep = 0; rep < 4; ++rep) {
+                T.start(s);
+                int rc = st_greedy(x, g, nullptr, n, d, ld, l, tr, Mr, idx, A, ws, ws_bytes, s);
+                if (rc) { fprintf(stderr, "rc=%d %s\n", rc, st_last_error()); exit(1); }
+                v.push_back(T.stop(s));
+            }
+            CK(hipMemcpy(h.data(), idx, 4 * Mr, hipMemcpyDeviceToHost));
+            if (ref.empty()) ref = h;
+            std::sort(v.begin(), v.end());
+            printf("replicas=%2d pitch=%4d  m=%d  best %8.3f ms  median %8.3f ms  (%6.2f us/step)  same_idx=%d\n",
+                   cfg.nrep, cfg.pitch, Mr, v[0], v[2], v[0] * 1e3 / Mr, (int)(h == ref));
+            fflush(stdout);
+        }
+        st_tune(10, -1); st_tune(9, -1);
+        return 0;
+    }
     // whole-run st_greedy: persistent kernel (register rows per thread rt; 0 = launch per step)
     struct V { int rt, nt; };
     for (V cfg : {V{8, 512}, V{6, 512}, V{4, 512}, V{16, 256}, V{0, 256}}) {
@@ -190,6 +216,7 @@ int main(int argc, char** argv) {
         if (getenv("PROBE_BPC")) st_tune(8, atoi(getenv("PROBE_BPC")));
         if (getenv("PROBE_NT")) st_tune(4, atoi(getenv("PROBE_NT")));
         if (getenv("PROBE_RT")) st_tune(3, atoi(getenv("PROBE_RT")));
+        if (getenv("PROBE_NREP")) st_tune(10, atoi(getenv("PROBE_NREP")));
         uint64_t* dst;
         CK(hipMalloc(&dst, sizeof(uint64_t) * GMAX * SP * PH));
         CK(hipMemset(dst, 0, sizeof(uint64_t) * GMAX * SP * PH));
