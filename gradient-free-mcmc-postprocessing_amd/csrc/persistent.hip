@@ -181,7 +181,7 @@ struct PersistArgs {
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
 // every block records s_memrealtime (100 MHz, chip-wide clock) at each phase of steps
 // [kStampFirst, kStampFirst + kStampSteps).
-[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 10;
+[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 20;
 #ifdef ST_PERSIST_STAMPS
 #define ST_STAMP(a, t, ph)                                                                         \
     do {                                                                                            \
@@ -195,7 +195,15 @@ struct PersistArgs {
         asm volatile("" ::"v"(val));                                                                \
         ST_STAMP(a, t, ph);                                                                         \
     } while (0)
+// per-wave stamp: lane 0 of every wave writes phase ph + wave
+#define ST_STAMP_WAVE(a, t, ph)                                                                    \
+    do {                                                                                            \
+        if ((a).stamps && (threadIdx.x & 63) == 0 && (t) >= kStampFirst && (t) < kStampFirst + kStampSteps) \
+            (a).stamps[((int64_t)blockIdx.x * kStampSteps + ((t) - kStampFirst)) * kStampPhases + (ph) + \
+                       (threadIdx.x >> 6)] = __builtin_amdgcn_s_memrealtime();                         \
+    } while (0)
 #else
+#define ST_STAMP_WAVE(a, t, ph) do { } while (0)
 #define ST_STAMP(a, t, ph) do { } while (0)
 #define ST_STAMP_AFTER(a, t, ph, val) do { } while (0)
 #endif
@@ -225,10 +233,13 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
     // padding rows (>= r1) carry +inf and the "no row" sentinel index, so they lose every tie --
     // their indices may be real rows of the next rank
     int64_t li = (int64_t)row < r1 ? (int64_t)row : INT64_MAX;
+    ST_STAMP_WAVE(a, t, 12);
     p_wave_minloc(v, li);
+    ST_STAMP_AFTER(a, t, 10, v);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     if (lane == 0) { sc->v[wave] = v; sc->i[wave] = li; }
     __syncthreads();
+    ST_STAMP(a, t, 11);
     if (a.nrep == 1) {
         if (threadIdx.x == 0) {   // ONE lane combines the wave minima and stores the two granules
             v = sc->v[0];

@@ -212,7 +212,7 @@ int main(int argc, char** argv) {
     st_tune(4, -1);
 #ifdef ST_PERSIST_STAMPS
     {   // phase breakdown of persistent steps 20..51 (s_memrealtime, 10 ns ticks)
-        const int SP = 32, PH = 10, GMAX = 512;
+        const int SP = 32, PH = 20, GMAX = 512;
         if (getenv("PROBE_BPC")) st_tune(8, atoi(getenv("PROBE_BPC")));
         if (getenv("PROBE_NT")) st_tune(4, atoi(getenv("PROBE_NT")));
         if (getenv("PROBE_RT")) st_tune(3, atoi(getenv("PROBE_RT")));
@@ -281,6 +281,27 @@ int main(int argc, char** argv) {
                    swt / its / 100);
             printf("sweep-done -> minloc-done %.2f us; winner row loaded after the sweep in %.0f%% of steps\n",
                    mloc / ((SP - 1) * G) / 100, tot > 0 ? 100.0 * late / tot : -1.0);
+        }
+        {   // publish breakdown: wave 0's compute end (3) -> its minloc (10); waves' compute ends
+            // (12 + w) -> spread; barrier passed (11); record stored (4)
+            double ml = 0, spread = 0, w0_to_last = 0, bar = 0, st = 0;
+            int cntp = 0;
+            const int NW = getenv("PROBE_NT") && atoi(getenv("PROBE_NT")) == 256 ? 4 : 8;
+            for (int stp = 1; stp < SP; ++stp)
+                for (int b = 0; b < G; ++b) {
+                    const uint64_t* q = &h[((size_t)b * SP + stp) * PH];
+                    uint64_t lo = ~(uint64_t)0, hi = 0;
+                    for (int w = 0; w < NW; ++w) { lo = std::min<uint64_t>(lo, q[12 + w]); hi = std::max<uint64_t>(hi, q[12 + w]); }
+                    ml += (double)(q[10] - q[12]);
+                    spread += (double)(hi - lo);
+                    w0_to_last += (double)(hi - q[12]);
+                    bar += (double)(q[11] - hi);
+                    st += (double)(q[4] - q[11]);
+                    ++cntp;
+                }
+            printf("publish split (us): wave0 minloc %.2f  waves' compute-end spread %.2f (wave0 -> last %.2f)  "
+                   "last wave end -> barrier passed %.2f  barrier -> record stored %.2f\n",
+                   ml / cntp / 100, spread / cntp / 100, w0_to_last / cntp / 100, bar / cntp / 100, st / cntp / 100);
         }
         printf("compute split (us): register rows %.2f  LDS rows %.2f  streamed rows %.2f\n",
                acc[7] / cnt / 100, ph_lds / cnt / 100, (acc[0] - acc[7] - ph_lds) / cnt / 100);
