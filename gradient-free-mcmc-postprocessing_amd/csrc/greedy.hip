@@ -252,7 +252,7 @@ __global__ __launch_bounds__(kBlock) void greedy_step_ct(GreedyArgs a) {
 // ------------------------------------------------------------------------------------------
 // Runtime-d variant (any 1 <= d <= 128): one candidate per lane per iteration, selected row in LDS.
 // ------------------------------------------------------------------------------------------
-template <bool GF, bool DIAG>
+template <bool GF, bool DIAG, bool NTL>
 __global__ __launch_bounds__(kBlock, 4) void greedy_step_rt(GreedyArgs a) {
     __shared__ double s_row[2 * kMaxDim + 1];
     __shared__ double s_v[kWaves];
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(kBlock, 4) void greedy_step_rt(GreedyArgs a) {
         } else {
             const double ai = a.A[i];
             const double wi = GF ? a.w[i] : 1.0;
-            kv = d >= 8 ? pair_value_rt8(a.x + i, a.g + i, ld, s_row, s_row + d, d, l, l2, tr)
+            kv = d >= 8 ? pair_value_rt8<NTL>(a.x + i, a.g + i, ld, s_row, s_row + d, d, l, l2, tr)
                         : pair_value_rt(a.x + i, a.g + i, ld, s_row, s_row + d, 1, d, l, l2, tr);
             if constexpr (GF) kv = (kv * wi) * wj;
             kv = ai + 2.0 * kv;
@@ -492,6 +492,9 @@ static void launch_ct(const GreedyArgs& a, bool diag, int blocks, hipStream_t s)
     }
 }
 
+// bytes a step streams above which its column loads are non-temporal: 3/4 of the 256 MB MALL
+constexpr double kStreamNtBytes = 192e6;
+
 hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStream_t s) {
     switch (a.d) {
         case 1: launch_ct<1>(a, diag, blocks, s); return hipGetLastError();
@@ -506,11 +509,20 @@ hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStr
     }
     const bool gf = a.w != nullptr;
     if (diag) {
-        if (gf) greedy_step_rt<true, true><<<blocks, kBlock, 0, s>>>(a);
-        else greedy_step_rt<false, true><<<blocks, kBlock, 0, s>>>(a);
+        if (gf) greedy_step_rt<true, true, false><<<blocks, kBlock, 0, s>>>(a);
+        else greedy_step_rt<false, true, false><<<blocks, kBlock, 0, s>>>(a);
+        return hipGetLastError();
+    }
+    // non-temporal column loads once a step's columns outgrow the memory-side cache (stein_math.hpp
+    // stream_load): config 5 (412 MB per step) 77.0 -> 70.0 us per step
+    // (profiles/r02_step_rt_nt_ab.log); smaller shards keep default loads and re-hit the MALL
+    const bool ntl = (double)a.n * (16.0 * a.d + 24.0) > kStreamNtBytes;
+    if (gf) {
+        if (ntl) greedy_step_rt<true, false, true><<<blocks, kBlock, 0, s>>>(a);
+        else greedy_step_rt<true, false, false><<<blocks, kBlock, 0, s>>>(a);
     } else {
-        if (gf) greedy_step_rt<true, false><<<blocks, kBlock, 0, s>>>(a);
-        else greedy_step_rt<false, false><<<blocks, kBlock, 0, s>>>(a);
+        if (ntl) greedy_step_rt<false, false, true><<<blocks, kBlock, 0, s>>>(a);
+        else greedy_step_rt<false, false, false><<<blocks, kBlock, 0, s>>>(a);
     }
     return hipGetLastError();
 }

@@ -250,10 +250,21 @@ __device__ __forceinline__ double pair_value_rt(const double* __restrict__ xa,
     return finish_pair(qs, t1s, t2s, t3s, tr);
 }
 
+// Columns streamed once per step: non-temporal loads (`nt`) when a step's working set exceeds the
+// 256 MB memory-side cache (MALL) -- the config-5 pattern (412 MB) runs 71.8 -> 62.4 us per pass
+// (profiles/r02_mall_nt_probe.log) -- and default loads when it fits, so that the MALL serves the
+// next step (d = 4, n = 2e6: 160 MB per step, nt measured 4-40 % slower).
+template <bool NTL, typename T>
+__device__ __forceinline__ T stream_load(const T* p) {
+    if constexpr (NTL) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
 // Runtime d >= 8 (the high-dimensional streaming step): the candidate's coordinates are loaded
 // eight at a time (16 independent loads in flight per lane; 4 waves per SIMD hide the rest),
-// matching NumPy's pairwise_sum lane structure for t3 (r[k % 8]).
+// matching NumPy's pairwise_sum lane structure for t3 (r[k % 8]); NTL: non-temporal loads.
 // The selected point (xb, gb) is block-uniform (LDS broadcast reads).  Same bits as pair_value_rt.
+template <bool NTL>
 __device__ __forceinline__ double pair_value_rt8(const double* __restrict__ xa,
                                                 const double* __restrict__ ga, int64_t sa,
                                                 const double* xb, const double* gb, int d,
@@ -264,7 +275,10 @@ __device__ __forceinline__ double pair_value_rt8(const double* __restrict__ xa,
     for (int k0 = 0; k0 < full; k0 += 8) {
         double cx[8], cg[8];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) { cx[j] = xa[(k0 + j) * sa]; cg[j] = ga[(k0 + j) * sa]; }
+        for (int j = 0; j < 8; ++j) {
+            cx[j] = stream_load<NTL>(xa + (k0 + j) * sa);
+            cg[j] = stream_load<NTL>(ga + (k0 + j) * sa);
+        }
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
             const int k = k0 + j;
@@ -285,7 +299,7 @@ __device__ __forceinline__ double pair_value_rt8(const double* __restrict__ xa,
     }
     double t3s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     for (int k = full; k < d; ++k) {
-        const double xak = xa[k * sa], gak = ga[k * sa];
+        const double xak = stream_load<NTL>(xa + k * sa), gak = stream_load<NTL>(ga + k * sa);
         const double xbk = xb[k], gbk = gb[k];
         const double dl = xak - xbk;
         const double gd = gak - gbk;

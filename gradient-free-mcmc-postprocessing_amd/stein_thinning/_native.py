@@ -120,7 +120,9 @@ def lib() -> ctypes.CDLL:
         with _LOCK:
             if _LIB is None:
                 import torch  # noqa: F401  -- map torch's HIP runtime before ours resolves against it
-                _LIB = load_library()
+                # ST_HIP_LIB: another build of the same ABI (same-box A/B timing of a kernel change,
+                # scripts/ab_run.sh); the in-tree library otherwise
+                _LIB = load_library(os.environ.get('ST_HIP_LIB') or LIB_PATH)
     return _LIB
 
 

@@ -5,6 +5,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
+if [[ -z ${1:-} ]]; then
 for r in 1 2; do
   timeout -k 10 120 ./tools/_diag/ab/probe 2000000 r > gpurun_out/ab_A_$r.log 2>&1 || exit 1
   timeout -k 10 120 ./tools/probe 2000000 r > gpurun_out/ab_B_$r.log 2>&1 || exit 1
@@ -14,3 +15,33 @@ timeout -k 10 120 ./tools/probe 250000 r > gpurun_out/ab_B_s.log 2>&1 || exit 1
 for f in ab_A_1 ab_B_1 ab_A_2 ab_B_2 ab_A_s ab_B_s; do
   echo "## $f"; grep -h "replicas=16\|replicas= 1 " gpurun_out/$f.log
 done
+fi
+# mode 2 (ab_run.sh step): the launch-per-step kernels -- bench config 5 (d = 50 step kernel) through
+# either library (ST_HIP_LIB), and the d = 4 step-kernel sweep of tools/probe
+if [[ ${1:-} == step ]]; then
+  for r in 1 2; do
+    ST_HIP_LIB=tools/_diag/ab/libstein_hip.so timeout -k 10 300 python3 bench.py --config c5 --steps 3 --warmup 1 \
+      --no-cpu-baseline > gpurun_out/ab_c5_A_$r.log 2>&1 || exit 1
+    timeout -k 10 300 python3 bench.py --config c5 --steps 3 --warmup 1 --no-cpu-baseline > gpurun_out/ab_c5_B_$r.log 2>&1 || exit 1
+  done
+  timeout -k 10 200 ./tools/_diag/ab/probe 2000000 > gpurun_out/ab_step_A.log 2>&1 || exit 1
+  timeout -k 10 200 ./tools/probe 2000000 > gpurun_out/ab_step_B.log 2>&1 || exit 1
+  for f in ab_c5_A_1 ab_c5_B_1 ab_c5_A_2 ab_c5_B_2; do
+    echo "## $f"; python3 -c "import json,sys; d=json.loads([l for l in open('gpurun_out/$f.log') if l.startswith('{')][-1]); print(d['ms_per_step'], json.dumps(d.get('roofline'))[:400])"
+  done
+  for f in ab_step_A ab_step_B; do echo "## $f"; grep -h "greedy blocks" gpurun_out/$f.log; done
+fi
+# mode 3 (ab_run.sh proxy): the proxy producers through either library, Gaussian and Student-t
+if [[ ${1:-} == proxy ]]; then
+  for r in 1 2; do
+    for k in gauss t; do
+      ST_HIP_LIB=tools/_diag/ab/libstein_hip.so timeout -k 10 300 python3 bench.py --workload proxy --proxy-kind $k \
+        --steps 20 --warmup 3 --no-cpu-baseline > gpurun_out/ab_px_A_${k}_$r.log 2>&1 || exit 1
+      timeout -k 10 300 python3 bench.py --workload proxy --proxy-kind $k --steps 20 --warmup 3 --no-cpu-baseline \
+        > gpurun_out/ab_px_B_${k}_$r.log 2>&1 || exit 1
+    done
+  done
+  for f in gpurun_out/ab_px_[AB]_*.log; do
+    echo "## $f"; python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); r=d['roofline']; print(d['ms_per_step'], r.get('kernel_avg_us'), r.get('frac'))"
+  done
+fi
