@@ -148,8 +148,11 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
         }
         const int fast = __syncthreads_and(rok) & col_fast;
         const int cnt = (int)((a_stop - ac) < R ? (a_stop - ac) : R);
-        auto sweep = [&](auto fast_tag) {
-            constexpr bool FAST = decltype(fast_tag)::value;
+        // every row of a tile that ends at or before the block's first column precedes all its
+        // columns: no per-pair triangle predicate (only the diagonal tile keeps it)
+        const bool below = ac + cnt <= c0;
+        auto sweep = [&](auto fast_tag, auto below_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value, BELOW = decltype(below_tag)::value;
             asm volatile(";; colsum variant" ::);
             auto pair_at = [&](int e) -> double {
                 double xa[D], ga[D];
@@ -167,15 +170,24 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
 #pragma unroll
                 for (int u = 0; u < kColsumUnroll; ++u) kv[u] = pair_at(e + u);
 #pragma unroll
-                for (int u = 0; u < kColsumUnroll; ++u) acc = (ac + e + u < i) ? acc + kv[u] : acc;
+                for (int u = 0; u < kColsumUnroll; ++u) {
+                    if constexpr (BELOW) acc = acc + kv[u];
+                    else acc = (ac + e + u < i) ? acc + kv[u] : acc;
+                }
             }
             for (; e < cnt; ++e) {
                 const double kv = pair_at(e);
-                acc = (ac + e < i) ? acc + kv : acc;
+                if constexpr (BELOW) acc = acc + kv;
+                else acc = (ac + e < i) ? acc + kv : acc;
             }
         };
-        if (fast) sweep(std::true_type{});
-        else sweep(std::false_type{});
+        if (fast) {
+            if (below) sweep(std::true_type{}, std::true_type{});
+            else sweep(std::true_type{}, std::false_type{});
+        } else {
+            if (below) sweep(std::false_type{}, std::true_type{});
+            else sweep(std::false_type{}, std::false_type{});
+        }
     }
     if (live) p.csum[i] = acc;
 }
@@ -285,29 +297,61 @@ __global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
     const int64_t i = c0 + tid;
     const bool live = i < p.na;
     double ai[D];
+    int aok = 1;
 #pragma unroll
-    for (int k = 0; k < D; ++k) ai[k] = live ? p.a[k * p.lda + i] : 0.0;
+    for (int k = 0; k < D; ++k) {
+        ai[k] = live ? p.a[k * p.lda + i] : 0.0;
+        aok &= fast_range_ok(ai[k]);
+    }
     int64_t lo, b_stop;
     dist_range(p, c0, R, lo, b_stop);
     double acc = 0.0;
     for (int64_t bc = lo; bc < b_stop; bc += R) {
         __syncthreads();
         const int64_t bb = bc + tid;
+        int tok = aok;
         if (bb < b_stop) {
 #pragma unroll
-            for (int k = 0; k < D; ++k) sb[k][tid] = p.b[k * p.ldb + bb];
-        }
-        __syncthreads();
-        const int cnt = (int)((b_stop - bc) < R ? (b_stop - bc) : R);
-        for (int e = 0; e < cnt; ++e) {
-            double ss = 0.0;
-#pragma unroll
             for (int k = 0; k < D; ++k) {
-                const double dk = ai[k] - sb[k][e];
-                ss += dk * dk;
+                const double v = p.b[k * p.ldb + bb];
+                sb[k][tid] = v;
+                tok &= fast_range_ok(v);
             }
-            const double dist = __builtin_sqrt(ss);
-            acc = (!p.tri || bc + e < i) ? acc + dist : acc;
+        }
+        // block-uniform: every coordinate of the tile and the block's columns is 0 or in
+        // [2^-60, 2^60] (squared distances 0 or in [2^-224, 2^124]), and the whole tile lies below
+        // the block's first column (no triangle predicate per pair)
+        const bool fast = __syncthreads_and(tok) != 0;
+        const int cnt = (int)((b_stop - bc) < R ? (b_stop - bc) : R);
+        const bool below = !p.tri || bc + cnt <= c0;
+        auto tile = [&](auto fast_tag, auto below_tag) {
+            constexpr bool FAST = decltype(fast_tag)::value, BELOW = decltype(below_tag)::value;
+            for (int e = 0; e < cnt; ++e) {
+                double ss = 0.0;
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    const double dk = ai[k] - sb[k][e];
+                    ss += dk * dk;
+                }
+                double dist;
+                if constexpr (FAST) {
+                    // the compiler's sqrt sequence without its scaling (ss >= 2^-767) and class
+                    // fix-up (only 0 and inf): the same bits as __builtin_sqrt in this range
+                    double h;
+                    dist = ss == 0.0 ? 0.0 : fast_sqrt(ss, h);
+                } else {
+                    dist = __builtin_sqrt(ss);
+                }
+                if constexpr (BELOW) acc = acc + dist;
+                else acc = (!p.tri || bc + e < i) ? acc + dist : acc;
+            }
+        };
+        if (fast) {
+            if (below) tile(std::true_type{}, std::true_type{});
+            else tile(std::true_type{}, std::false_type{});
+        } else {
+            if (below) tile(std::false_type{}, std::true_type{});
+            else tile(std::false_type{}, std::false_type{});
         }
     }
     if (live) p.out[(int64_t)blockIdx.y * p.na + i] = acc;
