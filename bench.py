@@ -565,8 +565,9 @@ def main_energy(args):
                          'traffic': pmc_traffic('energy') if world == 1 else None,
                          'kernel': f'dist_colsum_kernel<{d}> (+ reduce / cumsum)', 'step_median_us': round(step_s * 1e6, 1),
                          'flop_per_pair': flop_pair,
-                         'note': 'per pair: d differences, squares and sums, one IEEE sqrt (a ~10-instruction '
-                                 'sequence on gfx950) and the accumulate; O(n d) bytes -- fp64 VALU-bound'},
+                         'note': 'per pair: d differences, squares and sums, one correctly rounded sqrt (the '
+                                 'range-guarded ~10-instruction sequence, one quarter-rate v_rsq_f64) and the '
+                                 'accumulate; O(n d) bytes -- fp64 VALU-bound'},
         }
         if not args.no_cpu_baseline:
             from oracle import stein_numpy as ref
