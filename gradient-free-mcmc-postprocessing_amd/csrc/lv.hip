@@ -407,19 +407,41 @@ __global__ __launch_bounds__(256) void lv_dense_kernel(LvArgs a) {
             const double2 v0 = r2[7 + 2 * c], v1 = r2[8 + 2 * c];
             Q[c][0] = v0.x; Q[c][1] = v0.y; Q[c][2] = v1.x; Q[c][3] = v1.y;
         }
-        for (int k = kb; k < ke; ++k) {
-            const double x = (a.t_eval[k] - t_old) * inv_hd;
+        // the observation (t_k, y_k) loads of the next two points are in flight while this pair
+        // computes (L2-served, shared by every parameter point: without the prefetch each
+        // iteration waited a full load latency at three waves per SIMD); same order of the sums
+        const double c0 = a.cinv[0], c1 = a.cinv[1], c2 = a.cinv[2], c3 = a.cinv[3];
+        auto obs = [&](int k, double& tk, double& o0, double& o1) {
+            const int kc = k < ke ? k : ke - 1;    // past the piece: a harmless reload, unused
+            tk = a.t_eval[kc];
+            o0 = a.y_obs[2 * kc];
+            o1 = a.y_obs[2 * kc + 1];
+        };
+        auto point = [&](double tk, double o0, double o1) {
+            const double x = (tk - t_old) * inv_hd;
             double u[10];
 #pragma unroll
             for (int c = 0; c < 10; ++c)
                 u[c] = __builtin_fma(x, __builtin_fma(x, __builtin_fma(x, __builtin_fma(x, Q[c][3], Q[c][2]),
                                                                        Q[c][1]), Q[c][0]), y[c]);
-            const double r0 = a.y_obs[2 * k] - u[0], r1 = a.y_obs[2 * k + 1] - u[1];
-            const double g0 = a.cinv[0] * r0 + a.cinv[1] * r1;
-            const double g1 = a.cinv[2] * r0 + a.cinv[3] * r1;
+            const double r0 = o0 - u[0], r1 = o1 - u[1];
+            const double g0 = c0 * r0 + c1 * r1;
+            const double g1 = c2 * r0 + c3 * r1;
 #pragma unroll
             for (int j = 0; j < 4; ++j) acc[j] += u[2 + j] * g0 + u[6 + j] * g1;
+        };
+        double ta, a0, a1, tb, b0, b1;
+        obs(kb, ta, a0, a1);
+        obs(kb + 1, tb, b0, b1);
+        int k = kb;
+        for (; k + 1 < ke; k += 2) {
+            const double t0 = ta, p0 = a0, p1 = a1, t1 = tb, q0 = b0, q1 = b1;
+            obs(k + 2, ta, a0, a1);
+            obs(k + 3, tb, b0, b1);
+            point(t0, p0, p1);
+            point(t1, q0, q1);
         }
+        if (k < ke) point(ta, a0, a1);
     }
 #pragma unroll
     for (int j = 0; j < 4; ++j) {

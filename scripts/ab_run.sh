@@ -67,3 +67,14 @@ if [[ ${1:-} == ksd ]]; then
     echo "## $f"; python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); r=d['roofline']; print(d['ms_per_step'], r.get('kernel_avg_us'), r.get('frac'))"
   done
 fi
+# mode 6 (ab_run.sh lv): the LV gradient batch through either library
+if [[ ${1:-} == lv ]]; then
+  for r in 1 2; do
+    ST_HIP_LIB=tools/_diag/ab/libstein_hip.so timeout -k 10 300 python3 bench.py --workload lv --steps 5 --warmup 1 \
+      --no-cpu-baseline > gpurun_out/ab_lv_A_$r.log 2>&1 || exit 1
+    timeout -k 10 300 python3 bench.py --workload lv --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/ab_lv_B_$r.log 2>&1 || exit 1
+  done
+  for f in gpurun_out/ab_lv_[AB]_*.log; do
+    echo "## $f"; python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); r=d['roofline']; print(d['ms_per_step'], r.get('kernel_avg_us'), r.get('frac'))"
+  done
+fi
