@@ -394,7 +394,11 @@ __global__ __launch_bounds__(256) void lv_dense_kernel(LvArgs a) {
         const double2 h0 = r2[0], h1 = r2[1];
         const double t_old = h0.x, inv_hd = h0.y;
         const int kb = (int)h1.x + (lane - pstart[lo]) * P;
+#if defined(ST_LV_DIAG) && ST_LV_DIAG == 1   // diagnostic build: preamble and record loads only
+        const int ke = kb + 1;
+#else
         const int ke = kb + P < (int)h1.y ? kb + P : (int)h1.y;
+#endif
         double y[10], Q[10][4];
 #pragma unroll
         for (int c = 0; c < 10; c += 2) {
