@@ -57,11 +57,12 @@ if [[ ${1:-} == energy ]]; then
   done
 fi
 # mode 5 (ab_run.sh ksd): full-sample KSD column sums, config 2 (n = 2e5) through either library
-if [[ ${1:-} == ksd ]]; then
+if [[ ${1:-} == ksd || ${1:-} == ksdfull ]]; then
+  KF=""; [[ ${1:-} == ksdfull ]] && KF="--ksd-full"
   for r in 1 2; do
-    ST_HIP_LIB=tools/_diag/ab/libstein_hip.so timeout -k 10 300 python3 bench.py --workload ksd --steps 5 --warmup 1 \
+    ST_HIP_LIB=tools/_diag/ab/libstein_hip.so timeout -k 10 300 python3 bench.py --workload ksd $KF --steps 2 --warmup 1 \
       --no-cpu-baseline > gpurun_out/ab_ks_A_$r.log 2>&1 || exit 1
-    timeout -k 10 300 python3 bench.py --workload ksd --steps 5 --warmup 1 --no-cpu-baseline > gpurun_out/ab_ks_B_$r.log 2>&1 || exit 1
+    timeout -k 10 300 python3 bench.py --workload ksd $KF --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/ab_ks_B_$r.log 2>&1 || exit 1
   done
   for f in gpurun_out/ab_ks_[AB]_*.log; do
     echo "## $f"; python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); r=d['roofline']; print(d['ms_per_step'], r.get('kernel_avg_us'), r.get('frac'))"
