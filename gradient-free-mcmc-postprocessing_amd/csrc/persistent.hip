@@ -378,9 +378,21 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         };
         // one poll in flight (two staggered polls were measured slower at every stagger, with
         // and without replicas: profiles/r02_poll_stagger_rejected.log)
+        // While a poll is in flight the wave reduces what the earlier polls brought (wv, wi: the
+        // wave's best so far, uniform), so after the last poll only lanes whose best changed in it
+        // need combining -- usually none (the last records seldom hold the winner).
+        double wv = INFINITY;
+        int64_t wi = INT64_MAX;
         for (;;) {
             u32x4 qs[MAXG / 64];
             issue(qs);
+            if (it > 0) {   // no memory access: runs while the loads above are in flight
+                double rv = v;
+                int64_t ri = gi;
+                p_wave_minloc(rv, ri);
+                wv = rv;
+                wi = ri;
+            }
             take(qs);
             if (__all(seen == need)) break;
             if (!between()) break;
@@ -392,7 +404,20 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             a.stamps[((int64_t)blockIdx.x * kStampSteps + (t + 1 - kStampFirst)) * kStampPhases + 9] = it + 1;
 #endif
         int64_t my = gi;
-        p_wave_minloc(v, gi);
+        {   // lanes whose best beats the pre-reduced (wv, wi): none -> (wv, wi); one -> that lane's
+            // (it beats every other lane's best too); several, or no earlier reduction -> full minloc
+            const uint64_t bt = __builtin_amdgcn_ballot_w64(better(v, gi, wv, wi));
+            if (bt == 0) {
+                v = wv;
+                gi = wi;
+            } else if (__builtin_popcountll(bt) == 1) {
+                const int L = __builtin_ctzll(bt);
+                v = __longlong_as_double((long long)readlane_u64((uint64_t)__double_as_longlong(v), L));
+                gi = (int64_t)readlane_u64((uint64_t)gi, L);
+            } else {
+                p_wave_minloc(v, gi);
+            }
+        }
         ST_STAMP(a, t + 1, 7);
         if (a.nranks > 1 && ok_all) {
             // ---- rank level: push this rank's winner to every peer, gather the R winners ----
