@@ -79,3 +79,18 @@ if [[ ${1:-} == lv ]]; then
     echo "## $f"; python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); r=d['roofline']; print(d['ms_per_step'], r.get('kernel_avg_us'), r.get('frac'))"
   done
 fi
+# mode 7 (ab_run.sh ranks): same-device rehearsal of the multi-rank engine (2 and 4 processes on
+# the one GPU, ST_BENCH_SHARE_DEVICE=1) through either library
+if [[ ${1:-} == ranks ]]; then
+  for r in 1 2; do
+    for w in 2 4; do
+      ST_BENCH_SHARE_DEVICE=1 ST_HIP_LIB=$PWD/tools/_diag/ab/libstein_hip.so timeout -k 10 300 python3 bench.py --gpus $w \
+        --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/ab_rk_A_${w}_$r.log 2>&1 || exit 1
+      ST_BENCH_SHARE_DEVICE=1 timeout -k 10 300 python3 bench.py --gpus $w --steps 5 --warmup 2 --no-cpu-baseline \
+        > gpurun_out/ab_rk_B_${w}_$r.log 2>&1 || exit 1
+    done
+  done
+  for f in gpurun_out/ab_rk_[AB]_*.log; do
+    echo "## $f"; python3 -c "import json,sys; d=json.loads([l for l in open('$f') if l.startswith('{')][-1]); print(d['n_gpus'], d['ms_per_step'], d['config']['parallelism'], d.get('degraded'))"
+  done
+fi
