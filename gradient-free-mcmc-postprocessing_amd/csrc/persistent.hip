@@ -38,6 +38,11 @@ constexpr int kMaxGrid = 512;               // up to two blocks per CU on MI355X
 constexpr int kMaxRanks = kMailboxRanks;    // GPUs of one node
 constexpr uint64_t kTimeoutTicks = 200000000ull;   // s_memrealtime runs at 100 MHz: 2 s
 constexpr uint64_t kFirstRankTimeoutTicks = 1000000000ull;   // 10 s: peers' launch skew at step 0
+// one device, step 0: every block of the grid publishes its diagonal minimum microseconds after it
+// starts, so a record still missing after 100 ms means the grid is not co-resident (another
+// kernel holds CUs: the plain launch below cannot reserve them).  The run aborts early and the
+// host re-runs the thin on the launch-per-step path (DeviceProblem.greedy).
+constexpr uint64_t kFirstStepTimeoutTicks = 10000000ull;
 // wide variant (D > 8, instantiated for D = 50): one row per thread in registers and no LDS or
 // streamed rows -- only when a block's rows fit (R <= 256: shards up to 256 x #CU rows, e.g. one
 // rank of an 8-GPU config-5 run); the winner row is read from LDS inside the pair loop
@@ -320,6 +325,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         const uint64_t* bank = a.gran + ((t & 1) * a.nrep + (int)blockIdx.x % a.nrep) * a.rep_stride;
         const uint64_t want = step_tag(t);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+        const uint64_t wait_limit = (t == 0 && a.nranks == 1) ? kFirstStepTimeoutTicks : kTimeoutTicks;
         uint32_t need = 0;
 #pragma unroll
         for (int c = 0; c < MAXG / 64; ++c) need |= (lane + 64 * c < G) ? (1u << c) : 0u;
@@ -386,7 +392,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                 row_of = gi;
             }
             if ((it & 15) == 15) {
-                const bool late = __builtin_amdgcn_s_memrealtime() - t0 > kTimeoutTicks;
+                const bool late = __builtin_amdgcn_s_memrealtime() - t0 > wait_limit;
                 const bool other = __hip_atomic_load(a.status, __ATOMIC_RELAXED,
                                                      __HIP_MEMORY_SCOPE_AGENT) != 0;
                 if (__any(late || other)) { ok_all = 0; return false; }
@@ -974,6 +980,9 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     // coop-launch row).  The cooperative path also made the HIP runtime create a cooperative queue
     // whose exit-time teardown crashes when rocprofv3's tool has finalised HSA first
     // (profiles/r02_exit_crash_bisect.log); a rank that cannot make progress times out, it never hangs.
+    // The occupancy query cannot see kernels of other streams / processes: a grid that is not
+    // co-resident aborts at step 0 after kFirstStepTimeoutTicks and the host re-runs the thin on
+    // the launch-per-step kernels (DeviceProblem.greedy; tests/test_gpu_fallback.py provokes it).
     int dev = 0, cus = 0, per_cu = 0;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;

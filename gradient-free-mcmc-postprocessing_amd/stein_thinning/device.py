@@ -8,6 +8,7 @@ an argmin.
 """
 from __future__ import annotations
 
+import warnings
 from typing import Optional
 
 import numpy as np
@@ -90,13 +91,30 @@ class DeviceProblem:
             self.l, self.tr, int(n_points), nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
             ws.numel() * 8, nat.stream_handle()), 'st_greedy')
 
+    def greedy_steps_launch(self, n_points: int, idx, a, ws) -> None:
+        """Enqueue the whole greedy run on the launch-per-step kernels (st_greedy_steps: no
+        co-residency requirement, the same bits as the persistent kernel)."""
+        nat.check(nat.lib().st_greedy_steps(
+            nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.n, self.d, self.ld,
+            self.l, self.tr, 0, int(n_points), int(n_points), nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
+            ws.numel() * 8, nat.stream_handle()), 'st_greedy_steps')
+
     def greedy(self, n_points: int, return_sums: bool = False):
+        """The reference's _greedy_search on the device.  ``self.fallback`` is None when the
+        persistent launch completed, else why the run was repeated on the launch-per-step path
+        (its bounded waits expired: the grid was not co-resident next to other work)."""
         idx, a, ws = self.greedy_buffers(n_points)
         self.greedy_launch(n_points, idx, a, ws)
         out = idx.cpu().numpy().view(np.uint32).copy()
+        self.fallback = None
         if out.size and int(out.max()) >= self.n:
-            raise nat.HipExtensionError('greedy kernel did not complete (persistent-kernel wait timed '
-                                        'out); indices poisoned')
+            self.fallback = ('persistent greedy kernel timed out (grid not co-resident?); '
+                             're-ran on the launch-per-step kernels')
+            warnings.warn(self.fallback, RuntimeWarning, stacklevel=2)
+            self.greedy_steps_launch(n_points, idx, a, ws)
+            out = idx.cpu().numpy().view(np.uint32).copy()
+            if out.size and int(out.max()) >= self.n:
+                raise nat.HipExtensionError('greedy step kernels returned out-of-range indices')
         if return_sums:
             return out, a[:self.n].cpu().numpy()
         return out
@@ -109,10 +127,17 @@ class DeviceProblem:
             return np.empty(0, dtype=np.float64)
         t1 = torch.from_numpy(np.ascontiguousarray(i1, dtype=np.int64)).to(self.device)
         t2 = torch.from_numpy(np.ascontiguousarray(i2, dtype=np.int64)).to(self.device)
+        return self.pairs_device(t1, t2)
+
+    def pairs_device(self, t1, t2) -> np.ndarray:
+        """k(row t1[q], row t2[q]) for index vectors already on the device (int64, rows < ld)."""
+        import torch
+        L = int(t1.shape[0])
         out = torch.empty(L, dtype=torch.float64, device=self.device)
-        nat.check(nat.lib().st_kernel_pairs(
-            nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.ld, self.d, self.l, self.tr,
-            nat.ptr(t1), nat.ptr(t2), L, nat.ptr(out), nat.stream_handle()), 'st_kernel_pairs')
+        if L:
+            nat.check(nat.lib().st_kernel_pairs(
+                nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.ld, self.d, self.l, self.tr,
+                nat.ptr(t1), nat.ptr(t2), L, nat.ptr(out), nat.stream_handle()), 'st_kernel_pairs')
         return out.cpu().numpy()
 
     def subset(self, rows: np.ndarray) -> 'DeviceProblem':

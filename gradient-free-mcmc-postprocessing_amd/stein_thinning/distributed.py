@@ -630,6 +630,32 @@ def _engine_runner(integrand: SteinIntegrand, n_points: int, group, use_graph: b
     return runner
 
 
+def _problem_digest(integrand: SteinIntegrand, n_points: int) -> np.ndarray:
+    """Cheap fingerprint of a thinning problem: shape, m, preconditioner and 4 096 evenly spaced
+    standardised rows (+ weights).  Ranks running independent thins (different chains) differ."""
+    n = integrand.n
+    rows = np.linspace(0, n - 1, min(n, 4096)).astype(np.int64)
+    parts = [np.array([n, integrand.sample.shape[1], n_points, integrand.weights is not None], dtype=np.int64),
+             np.array([integrand.linv_scale, integrand.linv_trace]),
+             integrand.sample[rows], integrand.gradient[rows]]
+    if integrand.weights is not None:
+        parts.append(integrand.weights[rows])
+    return np.concatenate([np.ascontiguousarray(p).view(np.uint8).reshape(-1) for p in parts])
+
+
+def thin_across_ranks(integrand: SteinIntegrand, n_points: int, group=None) -> np.ndarray:
+    """The drop-in ``thin`` / ``thin_gf`` under a multi-rank launch (``thinning._greedy_search``
+    routes here when torch.distributed is initialised with world > 1): the candidate rows are
+    sharded over the ranks exactly as ``thin_sharded`` does, and every rank returns the
+    single-process indices.  Collective: every rank must call it with the same problem -- checked
+    first; ranks thinning different samples (the reference's per-chain fan-out,
+    ``code/src/utils/parallel.py:48-52``) get a ValueError and should set ST_SHARD_THIN=0."""
+    if not _group_same(_problem_digest(integrand, n_points), group):
+        raise ValueError('thin() under torch.distributed: the ranks hold different problems; '
+                         'set ST_SHARD_THIN=0 to thin independently on every rank')
+    return _thin_sharded_integrand(integrand, n_points, group)
+
+
 def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None,
                             use_graph: bool = True) -> np.ndarray:
     n_points = int(n_points)

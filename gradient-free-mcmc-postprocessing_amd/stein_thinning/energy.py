@@ -64,42 +64,99 @@ def _check(x, y):
         raise ValueError('energy distance of an empty sample')
 
 
+class PointSet:
+    """A point set resident on the GPU (SoA) with its self term sum_{a<b} |p_a - p_b| computed on
+    first use and kept: the reference scores every method and chain against ONE validation
+    sample (``Comparison.ipynb`` cells 19-23: ``fit_quality`` per method x chain), and that
+    sample's n_v^2 / 2 triangle is ~99 % of a curve's distance evaluations."""
+
+    def __init__(self, points: np.ndarray, device):
+        self.host = np.array(points, dtype=np.float64, copy=True)
+        self.device = device
+        self.soa, self.n, self.d, self.ld = _soa(self.host, device)
+        self._self_sum = None
+
+    def self_sum(self, recompute: bool = False):
+        """Device scalar sum over a < b of |p_a - p_b| (cached unless ``recompute``)."""
+        if self._self_sum is None or recompute:
+            s = _colsum(self.soa, self.n, self.ld, self.soa, self.n, self.ld, self.d, 0, self.n, True,
+                        self.device, host=False).sum()
+            if recompute:
+                return s
+            self._self_sum = s
+        return self._self_sum
+
+    def holds(self, points: np.ndarray, device) -> bool:
+        return device == self.device and points.shape == self.host.shape and np.array_equal(points, self.host)
+
+
+_SETS: list = []          # most recently used first
+_SETS_MAX = 4
+_SETS_MIN_ROWS = 4096     # smaller sets: the comparison would cost about as much as the self term
+
+
+def point_set(points, device=None, cache: bool = True) -> PointSet:
+    """The resident PointSet holding exactly these values (re-used across calls: its self term is
+    computed once), or a new one.  Values are compared on every lookup, so an array changed in
+    place is never served from a stale copy."""
+    pts = _points(points)
+    dev = device if device is not None else nat.require_device()
+    if not cache or pts.shape[0] < _SETS_MIN_ROWS:
+        return PointSet(pts, dev)
+    for k, e in enumerate(_SETS):
+        if e.holds(pts, dev):
+            if k:
+                _SETS.insert(0, _SETS.pop(k))
+            return e
+    e = PointSet(pts, dev)
+    _SETS.insert(0, e)
+    del _SETS[_SETS_MAX:]
+    return e
+
+
 def energy_distance(x, y) -> float:
-    """dcor.energy_distance(x, y) (V-statistic, exponent 1), evaluated on the GPU."""
+    """dcor.energy_distance(x, y) (V-statistic, exponent 1), evaluated on the GPU.  A large point
+    set seen before (the validation sample of every fit_quality call) re-uses its self term."""
     x, y = _points(x), _points(y)
     _check(x, y)
     dev = nat.require_device()
-    xs, nx, d, ldx = _soa(x, dev)
-    ys, ny, _, ldy = _soa(y, dev)
-    cross = _colsum(xs, nx, ldx, ys, ny, ldy, d, 0, ny, False, dev).sum()
-    xx = _colsum(xs, nx, ldx, xs, nx, ldx, d, 0, nx, True, dev).sum()
-    yy = _colsum(ys, ny, ldy, ys, ny, ldy, d, 0, ny, True, dev).sum()
+    xp, yp = point_set(x, dev), point_set(y, dev)
+    cross = _colsum(xp.soa, xp.n, xp.ld, yp.soa, yp.n, yp.ld, xp.d, 0, yp.n, False, dev).sum()
+    xx = float(xp.self_sum().item())
+    yy = float(yp.self_sum().item())
+    nx, ny = xp.n, yp.n
     return float(2.0 * cross / (nx * ny) - 2.0 * xx / (nx * nx) - 2.0 * yy / (ny * ny))
 
 
 class EnergyCurve:
     """The reference's fit_quality curve, sqrt(ED(reference_points, sample[idx[:k]])) for every k in
     ``sizes`` (Comparison.ipynb cells 19-23), with both point sets resident on the GPU: the
-    reference set's self term once, the cross sums once per selected point, the selection's self
-    sums once (instead of one full dcor evaluation per prefix)."""
+    reference set's self term once per reference set (``PointSet``: shared by every curve against
+    the same validation sample; ``cache_reference=False`` recomputes it in every launch), the
+    cross sums once per selected point, the selection's self sums once (instead of one full dcor
+    evaluation per prefix)."""
 
-    def __init__(self, reference_points, selection):
-        x, y = _points(reference_points), _points(selection)
-        _check(x, y)
+    def __init__(self, reference_points, selection, cache_reference: bool = True):
+        y = _points(selection)
         self.device = nat.require_device()
-        self.xs, self.nx, self.d, self.ldx = _soa(x, self.device)
+        self.ref = reference_points if isinstance(reference_points, PointSet) else \
+            point_set(reference_points, self.device, cache=cache_reference)
+        _check(self.ref.host, y)
+        self.cache_reference = cache_reference
+        self.xs, self.nx, self.d, self.ldx = self.ref.soa, self.ref.n, self.ref.d, self.ref.ld
         self.ys, self.ny, _, self.ldy = _soa(y, self.device)
 
-    def pair_count(self) -> int:
-        """Distance evaluations per run: the reference set's triangle, the cross block, the
-        selection's triangle."""
-        return self.nx * (self.nx - 1) // 2 + self.nx * self.ny + self.ny * (self.ny - 1) // 2
+    def pair_count(self, include_reference: bool = True) -> int:
+        """Distance evaluations per run: the reference set's triangle (once per reference set when
+        cached), the cross block, the selection's triangle."""
+        ref = self.nx * (self.nx - 1) // 2 if include_reference else 0
+        return ref + self.nx * self.ny + self.ny * (self.ny - 1) // 2
 
     def launch(self, sizes):
         """Enqueue one curve evaluation (device tensors; no host sync)."""
         import torch
         dev, d = self.device, self.d
-        xx = _colsum(self.xs, self.nx, self.ldx, self.xs, self.nx, self.ldx, d, 0, self.nx, True, dev, host=False).sum()
+        xx = self.ref.self_sum(recompute=not self.cache_reference)
         cross = torch.cumsum(_colsum(self.ys, self.ny, self.ldy, self.xs, self.nx, self.ldx, d, 0, self.nx, False,
                                      dev, host=False), 0)                       # per selected point
         yy = torch.cumsum(_colsum(self.ys, self.ny, self.ldy, self.ys, self.ny, self.ldy, d, 0, self.ny, True,

@@ -98,7 +98,24 @@ def _record_rows(integrand: Callable, inner: SteinIntegrand, n: int) -> Optional
         return None
     if out.dtype != np.float64 or not np.array_equal(out, sent.reshape(-1)):
         return None
-    return r1.astype(np.int64)
+    rows = r1.astype(np.int64)
+    # second, independent probe (two random permutations): the map must hold for it too -- a
+    # wrapper that swaps its arguments (inner(perm[b], perm[a])) passes the reversed-arange probe
+    # with rows = perm[::-1] but fails here
+    rng = np.random.default_rng(0x5eed)
+    a2, b2 = rng.permutation(n), rng.permutation(n)
+    try:
+        with inner.recording() as rec:
+            out2 = np.asarray(integrand(a2, b2))
+    except Exception:   # noqa: BLE001
+        return None
+    if len(rec) != 1 or out2.shape != (n,):
+        return None
+    q1, q2, sent2 = rec[0]
+    if not (np.array_equal(q1, rows[a2]) and np.array_equal(q2, rows[b2])
+            and out2.dtype == np.float64 and np.array_equal(out2, sent2.reshape(-1))):
+        return None
+    return rows
 
 
 _trace_rows = _record_rows
@@ -145,6 +162,23 @@ def _row_blocks(n: int, start_pairs):
         i0 = i1
 
 
+_ELEMENTWISE_PREFIX = 8   # reference-loop rows compared against one batched call
+
+
+def _elementwise(integrand: Callable, calls) -> bool:
+    """True iff ONE call on the concatenated index arrays of ``calls`` (a few of the reference
+    loop's (ind1, ind2) calls) returns exactly what the separate calls return: only then may the
+    loop's calls be batched (a wrapper that uses ind1[0], len(ind2), or mixes elements is not
+    elementwise and keeps the per-row protocol)."""
+    try:
+        sep = [np.asarray(integrand(i1, i2), dtype=np.float64).reshape(-1) for i1, i2 in calls]
+        one = np.asarray(integrand(np.concatenate([c[0] for c in calls]), np.concatenate([c[1] for c in calls])),
+                         dtype=np.float64).reshape(-1)
+    except Exception:   # noqa: BLE001 -- not batchable: the reference loop raises or runs as it would
+        return False
+    return np.array_equal(one, np.concatenate(sep), equal_nan=True)
+
+
 def ksd(integrand: Callable, n: int) -> np.ndarray:
     """Cumulative KSD: ks[i] = sqrt(sum_{a,b <= i} k(a, b)) / (i + 1), i < n."""
     n = int(n)
@@ -155,7 +189,8 @@ def ksd(integrand: Callable, n: int) -> np.ndarray:
         return _problem(*dev).ksd(n)
     ks = np.empty(n)
     ps = 0.
-    if _inner_integrand(integrand) is not None:
+    if _inner_integrand(integrand) is not None and _elementwise(
+            integrand, [(np.full(i + 1, i), np.arange(i + 1)) for i in range(min(n, _ELEMENTWISE_PREFIX))]):
         # batched: the reference loop's calls for rows [i0, i1) as ONE call, summed per row in its order
         for i0, i1 in _row_blocks(n, lambda a, b: (b * (b + 1) - a * (a + 1)) // 2):
             lens = np.arange(i0, i1) + 1
@@ -183,7 +218,8 @@ def kmat(integrand: Callable, n: int) -> np.ndarray:
     if dev is not None:
         return _problem(*dev).kmat(n)
     res = None
-    if _inner_integrand(integrand) is not None and n > 0:
+    if _inner_integrand(integrand) is not None and n > 0 and _elementwise(
+            integrand, [(np.full(n - i, i), np.arange(i, n)) for i in range(min(n, 2))]):
         for i0, i1 in _row_blocks(n, lambda a, b: (b - a) * n - (b * (b - 1) - a * (a - 1)) // 2):
             ind1 = np.repeat(np.arange(i0, i1), n - np.arange(i0, i1))
             ind2 = np.concatenate([np.arange(i, n) for i in range(i0, i1)])

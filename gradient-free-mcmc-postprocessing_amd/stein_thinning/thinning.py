@@ -249,11 +249,27 @@ def _greedy_search_protocol(n_points: int, integrand: Callable) -> np.ndarray:
     return idx
 
 
+def _rank_sharding() -> bool:
+    """True when thin / thin_gf run under a multi-rank launch (torch.distributed initialised with
+    more than one rank, e.g. torchrun with one process per GPU) and ST_SHARD_THIN is not '0': the
+    candidate rows are then split across the ranks (every rank must make the same call)."""
+    import os
+    if os.environ.get('ST_SHARD_THIN', '1') == '0':
+        return False
+    try:
+        import torch.distributed as dist
+    except ImportError:
+        return False
+    return dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1
+
+
 def _greedy_search(n_points: int, integrand: Callable) -> np.ndarray:
     """Greedy KSD minimisation (Algorithm 3, report.tex:413-426); returns uint32 indices.
 
-    SteinIntegrand -> the whole m-step loop runs on the GPU (one fused kernel per step, no host
-    round trip).  Any other callable -> the reference protocol loop.
+    SteinIntegrand -> the whole m-step loop runs on the GPU (one persistent launch, or one fused
+    kernel per step; no host round trip); under a multi-rank launch its rows are sharded across
+    the ranks (stein_thinning.distributed.thin_across_ranks, same indices).  Any other callable ->
+    the reference protocol loop.
     """
     n_points = int(n_points)
     if n_points < 0:
@@ -261,6 +277,9 @@ def _greedy_search(n_points: int, integrand: Callable) -> np.ndarray:
     if n_points == 0:
         raise IndexError('index 0 is out of bounds for axis 0 with size 0')
     if isinstance(integrand, SteinIntegrand):
+        if integrand._base is None and _rank_sharding():
+            from .distributed import thin_across_ranks
+            return thin_across_ranks(integrand, n_points)
         return integrand.device_problem().greedy(n_points)
     return _greedy_search_protocol(n_points, integrand)
 

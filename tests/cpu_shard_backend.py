@@ -82,6 +82,14 @@ class CpuShardBackend:
         return self.idx.copy()
 
 
+def from_integrand(integrand, r0, r1, nranks, n_points, mailboxes=None, rank=0):
+    """Drop-in for stein_thinning.distributed.HipShardBackend(integrand, r0, r1, nranks, n_points):
+    lets a gloo test run the product's thin() -> thin_across_ranks -> sharded_runner chain on CPU."""
+    assert mailboxes is None
+    return CpuShardBackend(integrand.sample, integrand.gradient, integrand.weights, integrand.linv_scale,
+                           integrand.linv_trace, r0, r1, nranks, n_points)
+
+
 class CpuKsdBackend:
     """CPU stand-in for HipKsdBackend: column sums of the lower triangle over a row range with the
     C bit model's pair values (same per-column sequential order as the HIP kernel)."""

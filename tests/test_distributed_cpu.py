@@ -61,6 +61,51 @@ def test_sharded_equals_single_process(tmp_path, world, gf):
         np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}.npy'), want)
 
 
+def _dropin_worker(rank, world, port, m, out_dir, differ):
+    """The drop-in stein_thinning.thinning.thin / thin_gf called on every rank of a gloo group: rows
+    sharded across the ranks (thin_across_ranks), CPU stand-in for the HIP shard backend."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='rccl')
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from stein_thinning import distributed as sd
+        from stein_thinning import thinning as st
+        from tests import cpu_shard_backend
+        sd.HipShardBackend = cpu_shard_backend.from_integrand
+        x, g, log_p, log_q = _data(True)
+        if differ:
+            try:
+                st.thin(x + rank, g, m, preconditioner='med')
+            except ValueError as e:
+                np.save(os.path.join(out_dir, f'err{rank}.npy'), np.array(['different problems' in str(e)]))
+            return
+        idx = st.thin(x, g, m, preconditioner='med')
+        mode = sd.last_mode
+        idx_gf = st.thin_gf(x, log_p, log_q, g, m, preconditioner='med')
+        np.save(os.path.join(out_dir, f'idx{rank}.npy'), idx)
+        np.save(os.path.join(out_dir, f'gf{rank}.npy'), idx_gf)
+        np.save(os.path.join(out_dir, f'mode{rank}.npy'), np.array([mode]))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dropin_thin_shards_under_multi_rank_launch(tmp_path):
+    m, world = 30, 2
+    mp.spawn(_dropin_worker, args=(world, _free_port(), m, str(tmp_path), False), nprocs=world, join=True)
+    x, g, log_p, log_q = _data(True)
+    want = o.thin(x, g, m, preconditioner='med')
+    want_gf = o.thin_gf(x, log_p, log_q, g, m, preconditioner='med')
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}.npy'), want)
+        np.testing.assert_array_equal(np.load(tmp_path / f'gf{r}.npy'), want_gf)
+        assert str(np.load(tmp_path / f'mode{r}.npy')[0]) == 'records-all-gather'
+
+
+def test_dropin_thin_rejects_different_problems_per_rank(tmp_path):
+    mp.spawn(_dropin_worker, args=(2, _free_port(), 10, str(tmp_path), True), nprocs=2, join=True)
+    for r in range(2):
+        assert bool(np.load(tmp_path / f'err{r}.npy')[0])
+
+
 def test_shard_bounds_cover_rows():
     for n in [1, 7, 100, 2_000_001]:
         for world in [1, 2, 3, 8]:

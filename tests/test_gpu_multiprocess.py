@@ -126,6 +126,36 @@ def test_replicated_engine_processes_share_one_gpu(tmp_path):
             np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
 
 
+def _dropin_worker(rank, world, port, out_dir):
+    """The reference's call surface, unchanged, on every rank of a 2-process group: thin / thin_gf
+    shard their rows across the ranks (thinning._greedy_search -> distributed.thin_across_ranks)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from stein_thinning import distributed as sd
+        from stein_thinning import thinning as st
+        x, g, log_p, log_q = _data()
+        for run, gf in enumerate([False, True]):
+            sd.last_mode = None
+            idx = st.thin_gf(x, log_p, log_q, g, 80, preconditioner='med') if gf else \
+                st.thin(x, g, 80, preconditioner='med')
+            np.save(os.path.join(out_dir, f'idx{rank}_{run}.npy'), idx)
+            with open(os.path.join(out_dir, f'mode{rank}_{run}.txt'), 'w') as f:
+                f.write(str(sd.last_mode))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dropin_thin_shards_across_two_processes(tmp_path):
+    mp.spawn(_dropin_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for run, gf in enumerate([False, True]):
+        want = _want(gf)
+        for r in range(2):
+            assert (tmp_path / f'mode{r}_{run}.txt').read_text() == 'device-exchange'
+            np.testing.assert_array_equal(np.load(tmp_path / f'idx{r}_{run}.npy'), want)
+
+
 def test_single_rank_rccl_graph_capture(tmp_path):
     mp.spawn(_worker, args=(1, _free_port(), 'nccl', False, str(tmp_path)), nprocs=1, join=True)
     x, g, _, _ = _data()

@@ -479,6 +479,13 @@ def test_ksd_kmat_wrappers_run_one_device_launch(gm_gpu, monkeypatch):
     for k in calls:
         calls[k] = 0
     scaled = ss.ksd(lambda i, j: 0.5 * integ(idx[i], idx[j]), 200)
-    assert calls['ksd'] == 0 and calls['pairs'] == 1, calls
+    # the elementwise check (ss._ELEMENTWISE_PREFIX separate calls + one batched) and ONE batch
+    assert calls['ksd'] == 0 and calls['pairs'] == ss._ELEMENTWISE_PREFIX + 2, calls
     ref_int = o._make_stein_integrand(gm_gpu['sample'], gm_gpu['gradient'])
     np.testing.assert_allclose(scaled, o.ksd(lambda i, j: 0.5 * ref_int(idx[i], idx[j]), 200), rtol=1e-12)
+    # an argument-swapping wrapper is not a re-indexing of the same rows: evaluated as written
+    for k in calls:
+        calls[k] = 0
+    swapped = ss.ksd(lambda i, j: integ(idx[j], idx[i]), 200)
+    assert calls['ksd'] == 0, calls
+    np.testing.assert_allclose(swapped, o.ksd(lambda i, j: ref_int(idx[j], idx[i]), 200), rtol=1e-12)

@@ -160,3 +160,45 @@ def test_bit_model_powers_are_correctly_rounded():
     for got, e in ((e15, 1.5), (e25, 2.5)):
         want = np.array([_cr_pow(v, e) for v in edge])
         assert np.all(np.abs(got - want) <= np.spacing(want))
+
+
+# ------------------------------------------------------------------------------------------
+# BASELINE configs 4 / 5 at full length: the C bit model (what the GPU parity tests compare the
+# running sums with) selects exactly the reference NumPy path's indices
+# (tests/golden/config{4,5}_numpy_indices.json, tests/golden/make_config_golden.py)
+# ------------------------------------------------------------------------------------------
+def _golden_config(name):
+    import json
+    import os
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', name)) as f:
+        return json.load(f)
+
+
+def _config_inputs(x, g, log_p=None, log_q=None):
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'med')
+    w = None if log_p is None else np.exp(o._log_weights(log_p, log_q, None))
+    return s, gs, w, float(linv[0, 0]), float(np.trace(linv))
+
+
+def test_bitmodel_config4_full_length_equals_numpy_fixture():
+    from bench import lv_surrogate
+    fx = _golden_config('config4_numpy_indices.json')
+    x, g, _, _ = lv_surrogate(2_000_000, 12345)
+    s, gs, _, l, tr = _config_inputs(x, g)
+    idx, _ = oracle_c.greedy_mt(s, gs, None, l, tr, 1000)
+    np.testing.assert_array_equal(idx, fx['indices'])
+    assert fx['min_margin_ulps'] > 1e3   # no step is a near tie that 1-ulp pow differences could flip
+
+
+def test_bitmodel_config5_full_length_equals_numpy_fixture():
+    import warnings
+    from bench import gaussian_d50
+    fx = _golden_config('config5_numpy_indices.json')
+    x, log_p, log_q, gq = gaussian_d50(500_000, 12349)
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        s, gs, w, l, tr = _config_inputs(x, gq, log_p, log_q)
+    idx, _ = oracle_c.greedy_mt(s, gs, w, l, tr, 500)
+    np.testing.assert_array_equal(idx, fx['indices'])
+    assert fx['min_margin_ulps'] > 1e3

@@ -154,6 +154,23 @@ def test_reindex_wrappers_are_traced_without_gpu():
     assert ss._record_rows(lambda i, j: integ(idx[i], idx[j]) + integ(idx[i], idx[j]), integ, n) is None
     assert ss._inner_integrand(lambda i, j: integ(i, j) - other(i, j)) is None
     assert ss._inner_integrand(lambda a, b: a) is None
+    # argument-swapping wrapper: passes the reversed-arange probe with rows = idx[::-1]
+    # but not the random-permutation probe, so it is not traced (the batched path evaluates it)
+    assert ss._record_rows(lambda a, b: integ(idx[b], idx[a]), integ, n) is None
+
+
+def test_batching_requires_an_elementwise_wrapper():
+    """stein.ksd / kmat batch the reference loop's calls only for wrappers that are elementwise over
+    the index arrays: a wrapper that uses ind1[0] or len(ind2) keeps the per-row loop."""
+    s = np.random.default_rng(1).normal(size=(30, 2))
+    ref = o._make_stein_integrand(s, -s)
+    elementwise = lambda i, j: 0.5 * ref(i, j)           # noqa: E731
+    by_first = lambda i, j: 0.5 * ref(np.full(len(i), i[0]), j)   # noqa: E731
+    by_len = lambda i, j: ref(i, j) / len(j)              # noqa: E731
+    calls = [(np.full(k + 1, k), np.arange(k + 1)) for k in range(6)]
+    assert ss._elementwise(elementwise, calls)
+    assert not ss._elementwise(by_first, calls)
+    assert not ss._elementwise(by_len, calls)
 
 
 def test_device_path_refuses_without_gpu(biv):
