@@ -186,7 +186,7 @@ struct PersistArgs {
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
 // every block records s_memrealtime (100 MHz, chip-wide clock) at each phase of steps
 // [kStampFirst, kStampFirst + kStampSteps).
-[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 20;
+[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 24;
 #ifdef ST_PERSIST_STAMPS
 #define ST_STAMP(a, t, ph)                                                                         \
     do {                                                                                            \
@@ -407,6 +407,12 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         // need combining -- usually none (the last records seldom hold the winner).
         double wv = INFINITY;
         int64_t wi = INT64_MAX;
+#ifdef ST_PERSIST_STAMPS
+        // speculation study (diagnostic build only): the wave's best record after the first poll,
+        // how many records that poll saw, and the poll after which the best stopped changing
+        int64_t spec_first = -1, spec_prev = -2;
+        unsigned spec_seen0 = 0, spec_settle = 0;
+#endif
         for (;;) {
             u32x4 qs[MAXG / 64];
             issue(qs);
@@ -418,14 +424,33 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                 wi = ri;
             }
             take(qs);
+#ifdef ST_PERSIST_STAMPS
+            {
+                double sv = v;
+                int64_t si = gi;
+                p_wave_minloc(sv, si);
+                if (it == 0) {
+                    spec_first = si;
+#pragma unroll
+                    for (int c = 0; c < MAXG / 64; ++c)
+                        spec_seen0 += (unsigned)__builtin_popcountll(__builtin_amdgcn_ballot_w64((seen >> c) & 1u));
+                }
+                if (si != spec_prev) { spec_prev = si; spec_settle = it + 1; }
+            }
+#endif
             if (__all(seen == need)) break;
             if (!between()) break;
             __builtin_amdgcn_s_sleep(1);
         }
         ST_STAMP(a, t + 1, 1);
 #ifdef ST_PERSIST_STAMPS
-        if (a.stamps && lane == 0 && t + 1 >= kStampFirst && t + 1 < kStampFirst + kStampSteps)
-            a.stamps[((int64_t)blockIdx.x * kStampSteps + (t + 1 - kStampFirst)) * kStampPhases + 9] = it + 1;
+        if (a.stamps && lane == 0 && t + 1 >= kStampFirst && t + 1 < kStampFirst + kStampSteps) {
+            uint64_t* sq = a.stamps + ((int64_t)blockIdx.x * kStampSteps + (t + 1 - kStampFirst)) * kStampPhases;
+            sq[9] = it + 1;
+            sq[20] = spec_seen0;
+            sq[21] = spec_settle;
+            sq[22] = (uint64_t)spec_first;
+        }
 #endif
         int64_t my = gi;
         {   // lanes whose best beats the pre-reduced (wv, wi): none -> (wv, wi); one -> that lane's

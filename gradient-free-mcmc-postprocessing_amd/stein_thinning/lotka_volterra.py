@@ -93,7 +93,11 @@ def grad_log_posterior(theta, data: Optional[LvData] = None, rtol: float = RTOL,
                        max_steps: int = MAX_STEPS, chunk: int = 1 << 16) -> np.ndarray:
     """``grad_log_posterior`` of Sensitivity_analysis.ipynb cell 46 for every row of ``theta``
     ((n, 4) or (4,)): returns (n, 4).  Two-phase kernels (``st_lv_grad_log_posterior_ws``), at most
-    ``chunk`` points per launch (the step table is ~29 KB per point)."""
+    ``chunk`` points per launch (the step table is ~29 KB per point; fewer when device memory is
+    short).  A point whose integration takes more than 64 accepted steps is recomputed by the
+    single-phase kernel, whose sum over the observation times runs in time order instead of in
+    pieces: the two forms agree to rounding (1e-11 relative, tests/test_gpu_lv.py), both within the
+    1e-8 tolerance against scipy."""
     import torch
     data = reference_data() if data is None else data
     th = _points(theta)
@@ -106,6 +110,11 @@ def grad_log_posterior(theta, data: Optional[LvData] = None, rtol: float = RTOL,
     if n:
         L = nat.lib()
         thd, td, yd = (torch.from_numpy(a).to(dev) for a in (th, t, y))
+        # the step table is ~29 KB per point: cap a launch's points at a quarter of the free device
+        # memory (torch's caching allocator keeps the block for the next call)
+        per_point = int(L.st_lv_grad_workspace_bytes(1, t.size))
+        free, _ = torch.cuda.mem_get_info(dev)
+        chunk = min(int(chunk), max(1024, free // 4 // per_point))
         m = min(n, chunk)
         wb = int(L.st_lv_grad_workspace_bytes(m, t.size))
         work = torch.empty((wb + 7) // 8, dtype=torch.float64, device=dev)

@@ -212,7 +212,7 @@ int main(int argc, char** argv) {
     st_tune(4, -1);
 #ifdef ST_PERSIST_STAMPS
     {   // phase breakdown of persistent steps 20..51 (s_memrealtime, 10 ns ticks)
-        const int SP = 32, PH = 20, GMAX = 512;
+        const int SP = 32, PH = 24, GMAX = 512;
         if (getenv("PROBE_BPC")) st_tune(8, atoi(getenv("PROBE_BPC")));
         if (getenv("PROBE_NT")) st_tune(4, atoi(getenv("PROBE_NT")));
         if (getenv("PROBE_RT")) st_tune(3, atoi(getenv("PROBE_RT")));
@@ -305,6 +305,31 @@ int main(int argc, char** argv) {
         }
         printf("compute split (us): register rows %.2f  LDS rows %.2f  streamed rows %.2f\n",
                acc[7] / cnt / 100, ph_lds / cnt / 100, (acc[0] - acc[7] - ph_lds) / cnt / 100);
+        {   // speculation study: is the best record after a block's FIRST poll the step's winner?
+            std::vector<uint32_t> hidx(M);
+            CK(hipMemcpy(hidx.data(), idx, 4 * M, hipMemcpyDeviceToHost));
+            double seen0 = 0, hits = 0, tot = 0, settle_before_last = 0, polls = 0;
+            double hist[6] = {0};
+            for (int st = 1; st < SP; ++st) {
+                const int64_t t = st + 20 - 1;   // stamps row st holds the sweep that picked idx[t]
+                if (t >= M) break;
+                for (int b = 0; b < G; ++b) {
+                    const uint64_t* q = &h[((size_t)b * SP + st) * PH];
+                    seen0 += (double)q[20];
+                    hits += (int64_t)q[22] == (int64_t)hidx[t];
+                    const double np = (double)q[9];
+                    polls += np;
+                    settle_before_last += (double)q[21] < np;
+                    hist[std::min<int>(5, (int)q[21])] += 1;
+                    tot += 1;
+                }
+            }
+            printf("speculation: first poll sees %.1f of %d records; its best is the winner in %.1f%% of "
+                   "block-steps; polls %.2f; best settled before the last poll in %.1f%%; settle poll histogram "
+                   "1:%.1f%% 2:%.1f%% 3:%.1f%% 4:%.1f%% 5+:%.1f%%\n",
+                   seen0 / tot, G, 100 * hits / tot, polls / tot, 100 * settle_before_last / tot, 100 * hist[1] / tot,
+                   100 * hist[2] / tot, 100 * hist[3] / tot, 100 * hist[4] / tot, 100 * hist[5] / tot);
+        }
     }
 #endif
     T.start(s);
