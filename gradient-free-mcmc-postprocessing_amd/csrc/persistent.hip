@@ -53,8 +53,8 @@ __device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minl
 struct Scratch {          // small per-block scratch at the start of the dynamic LDS region
     double row[2 * kWideD + 2];   // winner row {x[d], g[d], w}
     double vblk;          // this block's last published minimum (NaN iff some row's A is NaN)
-    double v[kMaxPWaves];
-    int64_t i[kMaxPWaves];
+    uint64_t wk[kMaxPWaves]; // per-wave minima as value_key (publish), then
+    int64_t i[kMaxPWaves];   // their indices; i[0] also carries the step's winner to the block
     int abort;
     int rowfast;          // wide d: the winner row lies in the fast range (set by the fetching wave)
     int ctr[2];           // 512-thread blocks: per-step chunk counters (dynamic LDS / streamed rows)
@@ -232,33 +232,39 @@ constexpr int64_t kNt512MinRows = 1280;
 
 __device__ __forceinline__ uint64_t step_tag(int64_t t) { return (uint64_t)((t + 1) & 0xFF) << 56; }
 
-// the block's wave minima in np.argmin order; nanfree (the step ran the range-guarded arithmetic:
-// no A of the block can be NaN) compares with '<' / '==' and the index only, a three-level
-// dependency per wave instead of take_if_better's NaN-aware chain.  Used for 256-thread blocks
-// only: same-box A/B 4.36 -> 4.23 us per step at 2.5e5 rows (256 threads), but +1.8 % at 2e6 rows
-// with 512-thread blocks (profiles/r02_nanfree_combine_ab.log)
+// Block records carry the minimum as an order-preserving 64-bit KEY instead of its raw bits, so the
+// sweeping wave compares records with integer compares (no NaN classification per record):
+//   NaN -> 0 (np.argmin: NaN is the minimum), x >= +0 -> bits | 2^63, x < 0 -> ~bits,
+// with -0 taken as +0 (they compare equal).  Unsigned key order = np.argmin's value order; equal
+// keys tie on the lower index as before.  key_value inverts it (key 0 -> a NaN).
+__device__ __forceinline__ uint64_t value_key(double v) {
+    const uint64_t b = (uint64_t)__double_as_longlong(v == 0.0 ? 0.0 : v);
+    const uint64_t k = (b >> 63) ? ~b : (b | 0x8000000000000000ull);
+    return __builtin_isnan(v) ? 0ull : k;
+}
+__device__ __forceinline__ double key_value(uint64_t k) {
+    return __longlong_as_double((long long)((k >> 63) ? (k ^ 0x8000000000000000ull) : ~k));
+}
+
+// the block's wave minima in np.argmin order, as (value_key, index) with integer compares (no NaN
+// classification: value_key already orders NaN first and -0 with +0); one lane, NT / 64 - 1 steps
 template <int NT>
-__device__ __forceinline__ void combine_waves(const Scratch* sc, bool nanfree, double& v, int64_t& li) {
-    v = sc->v[0];
-    li = sc->i[0];
-    if (NT <= 256 && nanfree) {
+__device__ __forceinline__ void combine_waves(const Scratch* sc, uint64_t& k, uint32_t& li) {
+    k = sc->wk[0];
+    li = sc->i[0] == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)sc->i[0];
 #pragma unroll
-        for (int w = 1; w < NT / 64; ++w) {
-            const double ov = sc->v[w];
-            const int64_t oi = sc->i[w];
-            const bool tk = (ov < v) | ((ov == v) & (oi < li));
-            v = tk ? ov : v;
-            li = tk ? oi : li;
-        }
-    } else {
-#pragma unroll
-        for (int w = 1; w < NT / 64; ++w) take_if_better(sc->v[w], sc->i[w], v, li);
+    for (int w = 1; w < NT / 64; ++w) {
+        const uint64_t ok = sc->wk[w];
+        const uint32_t oi = sc->i[w] == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)sc->i[w];
+        const bool tk = (ok < k) | ((ok == k) & (oi < li));
+        k = tk ? ok : k;
+        li = tk ? oi : li;
     }
 }
 
 template <int NT>
 __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, uint32_t row,
-                                        int64_t t, int64_t r1, bool nanfree = false) {
+                                        int64_t t, int64_t r1) {
     // padding rows (>= r1) carry +inf and the "no row" sentinel index, so they lose every tie --
     // their indices may be real rows of the next rank
     int64_t li = (int64_t)row < r1 ? (int64_t)row : INT64_MAX;
@@ -266,32 +272,32 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
     p_wave_minloc(v, li);
     ST_STAMP_AFTER(a, t, 10, v);
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    if (lane == 0) { sc->v[wave] = v; sc->i[wave] = li; }
+    if (lane == 0) { sc->wk[wave] = value_key(v); sc->i[wave] = li; }
     __syncthreads();
     ST_STAMP(a, t, 11);
     if (a.nrep == 1) {
         if (threadIdx.x == 0) {   // ONE lane combines the wave minima and stores the two granules
-            combine_waves<NT>(sc, nanfree, v, li);
-            sc->vblk = v;   // read by every thread after wait_and_pick's barrier
+            uint64_t k;
+            uint32_t ib;
+            combine_waves<NT>(sc, k, ib);
+            sc->vblk = key_value(k);   // read by every thread after wait_and_pick's barrier
             uint64_t* gr = a.gran + (t & 1) * a.rep_stride + (int64_t)blockIdx.x * a.rec_stride;
             const uint64_t tag = step_tag(t);
-            const uint64_t vb = (uint64_t)__double_as_longlong(v);
-            const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
-            __hip_atomic_store(gr + 0, tag | (vb >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            __hip_atomic_store(gr + 1, tag | ((vb & 0xFFull) << 32) | ib, __ATOMIC_RELAXED,
+            __hip_atomic_store(gr + 0, tag | (k >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_store(gr + 1, tag | ((k & 0xFFull) << 32) | ib, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
         }
     } else if (threadIdx.x < 64) {
         // replicated records: wave 0 combines (every lane the same values from LDS) and lane r
         // stores the record into replica r as ONE 16-B sc1 store (both granules tagged: a torn
         // store fails the reader's tag check like two 8-B stores would)
-        combine_waves<NT>(sc, nanfree, v, li);
-        if (threadIdx.x == 0) sc->vblk = v;
+        uint64_t k;
+        uint32_t ib;
+        combine_waves<NT>(sc, k, ib);
+        if (threadIdx.x == 0) sc->vblk = key_value(k);
         if ((int)threadIdx.x < a.nrep) {
             const uint64_t tag = step_tag(t);
-            const uint64_t vb = (uint64_t)__double_as_longlong(v);
-            const uint32_t ib = li == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)li;
-            const uint64_t g0 = tag | (vb >> 8), g1 = tag | ((vb & 0xFFull) << 32) | ib;
+            const uint64_t g0 = tag | (k >> 8), g1 = tag | ((k & 0xFFull) << 32) | ib;
             const int64_t off = (((t & 1) * a.nrep + threadIdx.x) * a.rep_stride +
                                  (int64_t)blockIdx.x * a.rec_stride) * 8;
             const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.gran, 0, 0x7FFFFFFF, 0x00020000);
@@ -330,8 +336,15 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
 #pragma unroll
         for (int c = 0; c < MAXG / 64; ++c) need |= (lane + 64 * c < G) ? (1u << c) : 0u;
         uint32_t seen = 0;
-        double v = INFINITY;
-        int64_t gi = INT64_MAX;
+        // the lane's best record so far as (key, index): value_key order, ties on the lower index;
+        // "none" = the key of +inf with the no-row index (a padding block's record ties with it)
+        constexpr uint64_t kNoKey = 0xFFF0000000000000ull;
+        uint64_t bk = kNoKey;
+        uint32_t bi = 0xFFFFFFFFu;
+        auto lane_best = [&](double& v, int64_t& i) {
+            v = key_value(bk);
+            i = bi == 0xFFFFFFFFu ? INT64_MAX : (int64_t)bi;
+        };
         int64_t row_of = INT64_MAX;        // index whose row is in rowv
         double rowv[kRow];
 #pragma unroll
@@ -367,29 +380,29 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                                                               0, 16 /* sc1 */);
             }
         };
+        // branch-free: per record the two tag bytes, the key's two halves and one (key, index)
+        // compare -- integer work only (records carry value_key, see publish); a record already seen
+        // (or past G) is skipped by its mask bit, whatever the zeros it was re-read as
+        const uint32_t want8 = (uint32_t)(want >> 56);
         auto take = [&](const u32x4 (&qs)[MAXG / 64]) {
+            const uint32_t open = need & ~seen;
 #pragma unroll
             for (int c = 0; c < MAXG / 64; ++c) {
-                if ((need & ~seen) & (1u << c)) {
-                    const u32x4 q = qs[c];
-                    const uint64_t g0 = ((uint64_t)q.y << 32) | q.x;
-                    const uint64_t g1 = ((uint64_t)q.w << 32) | q.z;
-                    if (((g0 & 0xFF00000000000000ull) == want) & ((g1 & 0xFF00000000000000ull) == want)) {
-                        seen |= 1u << c;
-                        const double rv = __longlong_as_double(
-                            (long long)(((g0 & 0x00FFFFFFFFFFFFFFull) << 8) | ((g1 >> 32) & 0xFFull)));
-                        const uint32_t ib = (uint32_t)g1;
-                        const int64_t ri = ib == 0xFFFFFFFFu ? INT64_MAX : (int64_t)ib;
-                        if (better(rv, ri, v, gi)) { v = rv; gi = ri; }
-                    }
-                }
+                const u32x4 q = qs[c];
+                const bool ok = (bool)((open >> c) & 1u) & ((q.y >> 24) == want8) & ((q.w >> 24) == want8);
+                const uint64_t k = ((uint64_t)((q.y << 8) | (q.x >> 24)) << 32) | ((q.x << 8) | (q.w & 0xFFu));
+                const uint32_t ib = q.z;
+                const bool tk = ok & ((k < bk) | ((k == bk) & (ib < bi)));
+                bk = tk ? k : bk;
+                bi = tk ? ib : bi;
+                seen |= ok ? (1u << c) : 0u;
             }
         };
         // after a poll: speculative row of the best so far; every 16 polls the bounded-wait check
         auto between = [&]() -> bool {
-            if (gi != row_of && gi != INT64_MAX) {
-                load_row(gi);
-                row_of = gi;
+            if (bi != 0xFFFFFFFFu && (int64_t)bi != row_of) {
+                load_row((int64_t)bi);
+                row_of = (int64_t)bi;
             }
             if ((it & 15) == 15) {
                 const bool late = __builtin_amdgcn_s_memrealtime() - t0 > wait_limit;
@@ -412,22 +425,34 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
         // how many records that poll saw, and the poll after which the best stopped changing
         int64_t spec_first = -1, spec_prev = -2;
         unsigned spec_seen0 = 0, spec_settle = 0;
+        uint64_t proc_ticks = 0;   // sum over polls of (records processed) - (poll data landed)
 #endif
         for (;;) {
             u32x4 qs[MAXG / 64];
             issue(qs);
             if (it > 0) {   // no memory access: runs while the loads above are in flight
-                double rv = v;
-                int64_t ri = gi;
+                double rv;
+                int64_t ri;
+                lane_best(rv, ri);
                 p_wave_minloc(rv, ri);
                 wv = rv;
                 wi = ri;
             }
+#ifdef ST_PERSIST_STAMPS
+            __builtin_amdgcn_s_waitcnt(0);   // diagnostic only: the poll's data has landed here
+            const uint64_t tp0 = __builtin_amdgcn_s_memrealtime();
+#endif
             take(qs);
 #ifdef ST_PERSIST_STAMPS
             {
-                double sv = v;
-                int64_t si = gi;
+                const int allseen = __all(seen == need) ? 1 : 0;
+                asm volatile("" ::"v"(allseen));
+                proc_ticks += __builtin_amdgcn_s_memrealtime() - tp0;
+            }
+            {
+                double sv;
+                int64_t si;
+                lane_best(sv, si);
                 p_wave_minloc(sv, si);
                 if (it == 0) {
                     spec_first = si;
@@ -450,8 +475,12 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             sq[20] = spec_seen0;
             sq[21] = spec_settle;
             sq[22] = (uint64_t)spec_first;
+            sq[23] = proc_ticks;
         }
 #endif
+        double v;
+        int64_t gi;
+        lane_best(v, gi);
         int64_t my = gi;
         {   // lanes whose best beats the pre-reduced (wv, wi): none -> (wv, wi); one -> that lane's
             // (it beats every other lane's best too); several, or no earlier reduction -> full minloc
@@ -906,7 +935,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
         if (__builtin_amdgcn_readfirstlane(wfast)) sweep_rows(std::true_type{});
         else sweep_rows(std::false_type{});
         ST_STAMP(a, t, 3);
-        publish<NT>(a, sc, bv, bi, t, r1, __builtin_amdgcn_readfirstlane(wfast) != 0);
+        publish<NT>(a, sc, bv, bi, t, r1);
         ST_STAMP(a, t, 4);
     }
     int64_t done = t;   // idx[0 .. done-1) are written

@@ -308,7 +308,7 @@ int main(int argc, char** argv) {
         {   // speculation study: is the best record after a block's FIRST poll the step's winner?
             std::vector<uint32_t> hidx(M);
             CK(hipMemcpy(hidx.data(), idx, 4 * M, hipMemcpyDeviceToHost));
-            double seen0 = 0, hits = 0, tot = 0, settle_before_last = 0, polls = 0;
+            double seen0 = 0, hits = 0, tot = 0, settle_before_last = 0, polls = 0, proc = 0;
             double hist[6] = {0};
             for (int st = 1; st < SP; ++st) {
                 const int64_t t = st + 20 - 1;   // stamps row st holds the sweep that picked idx[t]
@@ -316,6 +316,7 @@ int main(int argc, char** argv) {
                 for (int b = 0; b < G; ++b) {
                     const uint64_t* q = &h[((size_t)b * SP + st) * PH];
                     seen0 += (double)q[20];
+                    proc += (double)q[23];
                     hits += (int64_t)q[22] == (int64_t)hidx[t];
                     const double np = (double)q[9];
                     polls += np;
@@ -324,6 +325,8 @@ int main(int argc, char** argv) {
                     tot += 1;
                 }
             }
+            printf("sweep processing: %.3f us per poll from data landed to records taken (polls %.2f)\n",
+                   proc / polls / 100, polls / tot);
             printf("speculation: first poll sees %.1f of %d records; its best is the winner in %.1f%% of "
                    "block-steps; polls %.2f; best settled before the last poll in %.1f%%; settle poll histogram "
                    "1:%.1f%% 2:%.1f%% 3:%.1f%% 4:%.1f%% 5+:%.1f%%\n",
