@@ -268,6 +268,45 @@ def test_config4_eight_ranks_share_one_gpu(tmp_path, config4):
         np.testing.assert_array_equal(np.load(tmp_path / f'c4idx{r}.npy'), config4['idx'])
 
 
+def _config5_worker(rank, world, port, out_dir, m):
+    """One of `world` ranks of config 5 (n = 5e5, d = 50, gradient-free) on the shared GPU through the
+    drop-in thin_gf; grids capped to 256 / world blocks, so each rank's 62 500 rows exceed the wide
+    persistent kernel's 256 rows per block and the launch-per-step engine with the mailbox exchange
+    kernel runs (on an 8-GPU node every rank has its own 256 CUs and the wide persistent kernel)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        import warnings
+        from bench import gaussian_d50
+        from stein_thinning import _native as nat
+        from stein_thinning import distributed as sd
+        from stein_thinning import thinning as st
+        assert nat.lib().st_tune(5, 256 // world) == 0
+        x, log_p, log_q, gq = gaussian_d50(500_000, 12349)
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            idx = st.thin_gf(x, log_p, log_q, gq, m, preconditioner='med')
+        np.save(os.path.join(out_dir, f'c5idx{rank}.npy'), idx)
+        with open(os.path.join(out_dir, f'c5mode{rank}.txt'), 'w') as f:
+            f.write(str(sd.last_mode))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_config5_eight_ranks_share_one_gpu(tmp_path):
+    """Config 5 split over 8 processes as one job: all 500 indices identical to
+    the reference NumPy path's (tests/golden/config5_numpy_indices.json) on every rank."""
+    import json
+    world, m = 8, 500
+    with open(os.path.join(os.path.dirname(os.path.abspath(__file__)), 'golden', 'config5_numpy_indices.json')) as f:
+        want = np.asarray(json.load(f)['indices'])
+    mp.spawn(_config5_worker, args=(world, _free_port(), str(tmp_path), m), nprocs=world, join=True)
+    for r in range(world):
+        assert (tmp_path / f'c5mode{r}.txt').read_text() == 'device-exchange-steps-graph'
+        np.testing.assert_array_equal(np.load(tmp_path / f'c5idx{r}.npy'), want)
+
+
 def test_sharded_supported_query_matches_launcher():
     """st_greedy_sharded_supported evaluates the persistent launcher's own eligibility: d = 2, 4 any
     shard; d = 50 only while a rank's block has at most 256 rows (so the grid cap st_tune key 5
