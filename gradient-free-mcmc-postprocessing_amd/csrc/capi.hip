@@ -60,6 +60,7 @@ st::GreedyArgs make_args(const double* x, const double* g, const double* w, int6
     a.n = n; a.ld = ld; a.d = d; a.l = l; a.tr = tr;
     a.row_offset = 0;
     a.rec_stride = st::cand_stride(d);
+    a.compact = st::arith_compact();
     return a;
 }
 

@@ -163,11 +163,14 @@ __device__ __forceinline__ void load_tile(const GreedyArgs& a, int64_t i0, Tile<
     }
 }
 
+// jok: the compact arithmetic is on and l, tr and the selected row are in range (pair_value_sel's
+// rule: a candidate row in range too -> compact, otherwise exact)
 template <int D, bool GF, bool DIAG, int CPT>
 __device__ __forceinline__ void eval_tile(const GreedyArgs& a, int64_t i0,
                                           const Tile<D, GF, DIAG, CPT>& t, const double (&xj)[D],
                                           const double (&gj)[D], double wj, double l, double l2,
-                                          double tr, double& best_v, int64_t& best_i) {
+                                          double m3l2, double tr, int jok, double& best_v,
+                                          int64_t& best_i) {
     double out[CPT];
 #pragma unroll
     for (int c = 0; c < CPT; ++c) {
@@ -176,14 +179,21 @@ __device__ __forceinline__ void eval_tile(const GreedyArgs& a, int64_t i0,
         for (int k = 0; k < D; ++k) gi[k] = t.g[k][c];
         double kv;
         if constexpr (DIAG) {
-            kv = diag_value_ct<D>(gi, tr);
+            int cok = jok;
+#pragma unroll
+            for (int k = 0; k < D; ++k) cok &= fast_range_ok(t.g[k][c]);
+            if (cok) {   // the diagonal's row check needs its x too (the DIAG tile carries only g)
+#pragma unroll
+                for (int k = 0; k < D; ++k) cok &= fast_range_ok(a.x[(int64_t)k * a.ld + i0 + c]);
+            }
+            kv = diag_value_sel<D>(cok, gi, tr);
             if constexpr (GF) kv = (kv * t.w[c]) * t.w[c];
             out[c] = kv;
         } else {
             double xi[D];
 #pragma unroll
             for (int k = 0; k < D; ++k) xi[k] = t.x[k][c];
-            kv = pair_value_ct<D>(xi, gi, xj, gj, l, l2, tr);
+            kv = pair_value_sel<D>(jok && row_in_range<D>(xi, gi), xi, gi, xj, gj, l, l2, m3l2, tr);
             if constexpr (GF) kv = (kv * t.w[c]) * wj;
             out[c] = t.a[c] + 2.0 * kv;
         }
@@ -228,7 +238,9 @@ __global__ __launch_bounds__(kBlock) void greedy_step_ct(GreedyArgs a) {
         for (int k = 0; k < D; ++k) { xj[k] = 0.0; gj[k] = 0.0; }
     }
 
-    const double l = a.l, l2 = a.l * a.l, tr = a.tr;
+    const double l = a.l, l2 = a.l * a.l, m3l2 = -3.0 * l2, tr = a.tr;
+    int jok = a.compact & scale_in_range(l, tr);
+    if constexpr (!DIAG) jok &= row_in_range<D>(xj, gj);
     double best_v = INFINITY;
     int64_t best_i = INT64_MAX;
     if constexpr (PF) {
@@ -236,14 +248,14 @@ __global__ __launch_bounds__(kBlock) void greedy_step_ct(GreedyArgs a) {
             const int64_t un = u + ustride;
             T nxt;
             if (un < nunits) load_tile<D, GF, DIAG, CPT>(a, un * CPT, nxt);
-            eval_tile<D, GF, DIAG, CPT>(a, u * CPT, cur, xj, gj, wj, l, l2, tr, best_v, best_i);
+            eval_tile<D, GF, DIAG, CPT>(a, u * CPT, cur, xj, gj, wj, l, l2, m3l2, tr, jok, best_v, best_i);
             cur = nxt;
             u = un;
         }
     } else {
         for (; u < nunits; u += ustride) {
             load_tile<D, GF, DIAG, CPT>(a, u * CPT, cur);
-            eval_tile<D, GF, DIAG, CPT>(a, u * CPT, cur, xj, gj, wj, l, l2, tr, best_v, best_i);
+            eval_tile<D, GF, DIAG, CPT>(a, u * CPT, cur, xj, gj, wj, l, l2, m3l2, tr, jok, best_v, best_i);
         }
     }
     write_block_record(a, best_v, best_i, s_v, s_i);
@@ -424,10 +436,14 @@ static int g_max_blocks = 256;
 static int g_cpt = -1;
 static int g_pf = -1;
 static int g_rt_max_blocks = kMaxBlocks;
+static int g_arith = 1;   // st_tune key 11
 constexpr int64_t kLargeShard = 1000000;
+
+int arith_compact() { return g_arith; }
 
 int tune(int key, int value) {
     switch (key) {
+        case 11: if (value < -1 || value > 1) return -1; g_arith = value < 0 ? 1 : value; return 0;
         case 6: if (value < 1 || value > kMaxBlocks) return -1; g_rt_max_blocks = value; return 0;
         case 0: if (value < 1 || value > kMaxBlocks) return -1; g_max_blocks = value; return 0;
         case 1: if (value != -1 && value != 1 && value != 2 && value != 4) return -1; g_cpt = value; return 0;

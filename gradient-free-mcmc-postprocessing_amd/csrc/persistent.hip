@@ -155,6 +155,20 @@ __device__ __forceinline__ double pair_value_wide(const double (&xi)[D], const d
     else return finish_pair(qs, t1s, t2s, t3s, tr);
 }
 
+// Pair arithmetic of one sweep variant (block-uniform choice per step):
+//   AR 0: exact, general (NaN / overflow semantics of NumPy)   AR 1: exact, range-guarded (same bits)
+//   AR 2: compact (every pair of the block-step in range)     AR 3: per pair, compact iff jok (l, tr and
+//         the winner in range) and this row in range, else exact general (pair_value_sel's rule)
+template <int D, int AR>
+__device__ __forceinline__ double pair_ar(const double (&xi)[D], const double (&gi)[D], const double* xj,
+                                          const double* gj, double l, double l2, double m3l2, double tr,
+                                          int jok) {
+    if constexpr (AR == 2) return pair_compact_ct<D>(xi, gi, xj, gj, l, m3l2, tr);
+    else if constexpr (AR == 3)
+        return pair_value_sel<D>(jok && row_in_range<D>(xi, gi), xi, gi, xj, gj, l, l2, m3l2, tr);
+    else return pair_value_ct<D, AR == 1>(xi, gi, xj, gj, l, l2, tr);
+}
+
 }  // namespace
 
 struct PersistArgs {
@@ -597,9 +611,11 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
 }
 
 // BPC = blocks per CU: 2 puts two 256-thread blocks on each CU (two waves per SIMD, RT <= 8
-// register rows each, every block its own record): the fp64 pipe issues from two waves
-template <int D, bool GF, int RT, int NT, int BPC>
+// register rows each, every block its own record): the fp64 pipe issues from two waves.
+// CMP: the compact arithmetic for pairs in range (stein_math.hpp pair_compact_ct; st_tune key 11).
+template <int D, bool GF, int RT, int NT, int BPC, bool CMP>
 __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
+    static_assert(!CMP || D <= kMaxCtDim, "compact arithmetic: d <= 8 only");
     constexpr int kPBlock = NT;
     constexpr int kMaxG = 256 * BPC;     // records swept per step
     constexpr bool kTwoWaves = NT >= 512 || BPC > 1;   // two waves per SIMD
@@ -622,7 +638,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     const int64_t r1 = (r0 + a.rows_per_block < a.row_end) ? r0 + a.rows_per_block : a.row_end;
     const int64_t lds_base = r0 + (int64_t)RT * kPBlock;
     const int64_t str_base = lds_base + RL;
-    const double l = a.l, l2 = a.l * a.l, tr = a.tr;
+    const double l = a.l, l2 = a.l * a.l, m3l2 = -3.0 * l2, tr = a.tr;
+    const int lok = CMP ? scale_in_range(l, tr) : 0;   // compact: the per-problem part of the rule
 
     // ---- stage the block's rows on chip ----------------------------------------------------
     // and decide whether every row of the block admits the range-guarded fast pair arithmetic
@@ -631,7 +648,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     double xr[RT > 0 ? RT : 1][D], gr[RT > 0 ? RT : 1][kWide ? 1 : D], ar[RT > 0 ? RT : 1];
     double* sgw = sx;
     double wr[(GF && RT > 0) ? RT : 1];
-    int rok = fast_range_ok(l) & (int)(l > 0.0) & (int)(tr > 0.0) & (int)(tr <= 0x1p64);
+    int rok = scale_in_range(l, tr);
 #pragma unroll
     for (int q = 0; q < RT; ++q) {
         const int64_t row = r0 + (int64_t)q * kPBlock + tid;
@@ -681,6 +698,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
 #pragma unroll
             for (int k = 0; k < D; ++k) gt[k] = sgw[k * kPBlock + tid];
             kv = diag_value_ct<D>(gt, tr);
+        } else if constexpr (CMP) {
+            kv = diag_value_sel<D>(lok && row_in_range<D>(xr[q], gr[q]), gr[q], tr);
         } else {
             kv = diag_value_ct<D>(gr[q], tr);
         }
@@ -691,20 +710,20 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     if constexpr (!kWide) {
         for (int e = tid; e < RL; e += kPBlock) {
             const int64_t row = lds_base + e;
-            double gi[D];
+            double gi[D], xi[D];
 #pragma unroll
-            for (int k = 0; k < D; ++k) gi[k] = sg[k * RL + e];
-            double kv = diag_value_ct<D>(gi, tr);
+            for (int k = 0; k < D; ++k) { gi[k] = sg[k * RL + e]; xi[k] = sx[k * RL + e]; }
+            double kv = CMP ? diag_value_sel<D>(lok && row_in_range<D>(xi, gi), gi, tr) : diag_value_ct<D>(gi, tr);
             if constexpr (GF) kv = (kv * sw[e]) * sw[e];
             kv = row < r1 ? kv : INFINITY;
             sa[e] = kv;
             scan_take(kv, (uint32_t)row, bv, bi);
         }
         for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
-            double gi[D];
+            double gi[D], xi[D];
 #pragma unroll
-            for (int k = 0; k < D; ++k) gi[k] = a.g[k * ld + row];
-            double kv = diag_value_ct<D>(gi, tr);
+            for (int k = 0; k < D; ++k) { gi[k] = a.g[k * ld + row]; xi[k] = a.x[k * ld + row]; }
+            double kv = CMP ? diag_value_sel<D>(lok && row_in_range<D>(xi, gi), gi, tr) : diag_value_ct<D>(gi, tr);
             if constexpr (GF) kv = (kv * a.w[row]) * a.w[row];
             a.A[row] = kv;
             scan_take(kv, (uint32_t)row, bv, bi);
@@ -729,20 +748,25 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
         // NaN-free scan -- valid while no A of this block is NaN: the block's last minimum is NaN
         // iff one is, and fast steps keep finite sums finite (|2k| < 2^191 per step)
         int wfast = (block_fast != 0) & (int)!__builtin_isnan(sc->vblk);
+        int jok = lok;   // compact, mixed sweep: l, tr and the winner row in range
         if constexpr (kWide) {
             wfast &= sc->rowfast;   // checked by the wave that fetched the row (no 2d reloads here)
         } else {
+            int rowok = 1;
 #pragma unroll
             for (int k = 0; k < D; ++k) {
                 xj_r[k] = uniform(sc->row[k]);
                 gj_r[k] = uniform(sc->row[D + k]);
-                wfast &= fast_range_ok(xj[k]) & fast_range_ok(gj[k]);
+                rowok &= fast_range_ok(xj[k]) & fast_range_ok(gj[k]);
             }
+            wfast &= rowok;
+            jok &= rowok;
         }
         const double wj = GF ? uniform(sc->row[2 * D]) : 1.0;
         // one block-uniform choice per step: range-guarded fast arithmetic or the general one
-        auto sweep_rows = [&](auto fast_tag) {
-            constexpr bool FAST = decltype(fast_tag)::value;
+        auto sweep_rows = [&](auto ar_tag) {
+            constexpr int AR = decltype(ar_tag)::value;
+            constexpr bool FAST = AR == 1 || AR == 2;   // in range, NaN-free block: fma update, '<' scan
             // opaque marker: keeps LLVM from if-converting the two variants into
             // compute-both-and-select (both are pure arithmetic over the register rows)
             asm volatile(";; sweep_rows variant" ::);
@@ -785,7 +809,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
 #pragma unroll
             for (int q = 0; q < RT; ++q) {
                 const int64_t row = r0 + (int64_t)q * kPBlock + tid;
-                double kv = pair_value_ct<D, FAST>(xr[q], gr[q], xj, gj, l, l2, tr);
+                double kv = pair_ar<D, AR>(xr[q], gr[q], xj, gj, l, l2, m3l2, tr, jok);
                 if constexpr (GF) kv = (kv * wr[q]) * wj;
                 // padding rows (zeros) keep A = +inf: in the fast range k is finite, so
                 // inf + 2k = inf needs no mask; the general path masks the update instead
@@ -809,7 +833,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                 double xi[D], gi[D];
 #pragma unroll
                 for (int k = 0; k < D; ++k) { xi[k] = sx[k * RL + e]; gi[k] = sg[k * RL + e]; }
-                double kv = pair_value_ct<D, FAST>(xi, gi, xj, gj, l, l2, tr);
+                double kv = pair_ar<D, AR>(xi, gi, xj, gj, l, l2, m3l2, tr, jok);
                 if constexpr (GF) kv = (kv * sw[e]) * wj;
                 double av;
                 if constexpr (FAST) av = add_twice<true>(sa[e], kv);
@@ -819,7 +843,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             };
             // streamed rows: two per iteration, the next two rows' loads in flight meanwhile
             auto stream_pair = [&](const SRow& r) -> double {
-                double kv = pair_value_ct<D, FAST>(r.x, r.g, xj, gj, l, l2, tr);
+                double kv = pair_ar<D, AR>(r.x, r.g, xj, gj, l, l2, m3l2, tr, jok);
                 if constexpr (GF) kv = (kv * r.w) * wj;
                 return add_twice<FAST>(r.a, kv);
             };
@@ -932,8 +956,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
         };
         // the flag is block-uniform (same LDS row, same block flag): make that explicit so the
         // branch is scalar and the two variants stay separate code paths
-        if (__builtin_amdgcn_readfirstlane(wfast)) sweep_rows(std::true_type{});
-        else sweep_rows(std::false_type{});
+        if (__builtin_amdgcn_readfirstlane(wfast)) sweep_rows(std::integral_constant<int, CMP ? 2 : 1>{});
+        else sweep_rows(std::integral_constant<int, CMP ? 3 : 0>{});
         ST_STAMP(a, t, 3);
         publish<NT>(a, sc, bv, bi, t, r1);
         ST_STAMP(a, t, 4);
@@ -1024,7 +1048,9 @@ int persistent_tune(int key, int value) {
 
 template <int D, bool GF, int RT, int NT, int BPC = 1>
 static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s, bool dry) {
-    auto fn = greedy_persistent<D, GF, RT, NT, BPC>;
+    // the compact instantiation for d <= 8 when st_tune key 11 selects it (the default)
+    auto fn = (D <= kMaxCtDim && arith_compact()) ? greedy_persistent<D, GF, RT, NT, BPC, D <= kMaxCtDim>
+                                                  : greedy_persistent<D, GF, RT, NT, BPC, false>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;

@@ -57,9 +57,12 @@ struct GreedyArgs {
     double* recs_out;     // one record per block of this launch
     uint32_t* idx_out;    // device index array; launch t writes idx[t-1]
     int64_t t;            // step being computed (0 = diagonal)
+    int compact;          // 1: the compact arithmetic for pairs in range (d <= 8; stein_math.hpp)
 };
 
 int greedy_blocks(int64_t n, int d);
+// st_tune key 11: arithmetic of the d <= 8 greedy kernels (1 = compact, the default; 0 = exact)
+int arith_compact();
 int tune(int key, int value);
 int persistent_tune(int key, int value);
 int64_t persistent_ws_bytes(int d, int G, int rec_stride, int nrep);

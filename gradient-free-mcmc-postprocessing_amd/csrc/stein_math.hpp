@@ -140,6 +140,66 @@ __device__ __forceinline__ double finish_pair_fast(double qs, double t1s, double
     return (t1 + t2) + t3;
 }
 
+// ---- compact arithmetic (d <= 8 greedy kernels; default since round 3) --------------------------
+// The same kernel value by the shortest route that stays a few ulps from NumPy's evaluation
+// (bit model: oracle/stein_ref.c pair_compact; pinned to every reference fixture in
+// tests/test_oracle_compact.py).  With S = SEQ_FMA dk^2, G = SEQ_FMA (gi_k - gj_k) dk,
+// P = SEQ_FMA gi_k gj_k (first term a product, then one fma per coordinate):
+//   qf = fma(l, S, 1),  y = RN(1 / RN(sqrt(qf))),  k = y * fma(y^2, fma(y^2, fl(-3 l^2) S, fma(l, G, tr)), P)
+// i.e. t3 + t2 + t1 = P / qf^0.5 + (tr + l G) / qf^1.5 - 3 l^2 S / qf^2.5 regrouped around one
+// reciprocal square root: 20 + 23 fp64 instructions per pair at d = 4 instead of 101.  Applies to a
+// pair only when both rows are in the fast range (row_in_range) and l, tr are (the same guard as
+// finish_pair_fast: qf in [1, 2^185], nothing overflows or underflows); other pairs take the exact
+// arithmetic -- a per-pair rule, so the result does not depend on how rows are split over blocks,
+// kernels or ranks.  y is correctly rounded: fast_sqrt is the IEEE sqrt in this range and recip2
+// from its h is RN(1/s) (above).
+template <int D>
+__device__ __forceinline__ double pair_compact_ct(const double (&xi)[D], const double (&gi)[D],
+                                                  const double* xj, const double* gj, double l,
+                                                  double m3l2, double tr) {
+    double S = 0.0, G = 0.0, P = 0.0;
+#pragma unroll
+    for (int k = 0; k < D; ++k) {
+        const double dl = xi[k] - xj[k];
+        const double gd = gi[k] - gj[k];
+        if (k == 0) {
+            S = dl * dl; G = gd * dl; P = gi[0] * gj[0];
+        } else {
+            S = __builtin_fma(dl, dl, S); G = __builtin_fma(gd, dl, G); P = __builtin_fma(gi[k], gj[k], P);
+        }
+    }
+    const double q = __builtin_fma(l, S, 1.0);
+    double h;
+    const double s = fast_sqrt(q, h);
+    const double y = recip2(s, h + h);
+    const double y2 = y * y;
+    const double in = __builtin_fma(y2, m3l2 * S, __builtin_fma(l, G, tr));
+    return y * __builtin_fma(y2, in, P);
+}
+
+// k(x, x) in the compact arithmetic: S = G = 0, qf = 1, y = 1 -> fl(tr + P)
+template <int D>
+__device__ __forceinline__ double diag_compact_ct(const double (&gi)[D], double tr) {
+    double P = gi[0] * gi[0];
+#pragma unroll
+    for (int k = 1; k < D; ++k) P = __builtin_fma(gi[k], gi[k], P);
+    return tr + P;
+}
+
+// 1 if every coordinate of the row (x and g) is 0 or of magnitude in [2^-60, 2^60]
+template <int D>
+__device__ __forceinline__ int row_in_range(const double (&xi)[D], const double (&gi)[D]) {
+    int ok = 1;
+#pragma unroll
+    for (int k = 0; k < D; ++k) ok &= fast_range_ok(xi[k]) & fast_range_ok(gi[k]);
+    return ok;
+}
+
+// l and tr admit the fast / compact arithmetic (the kernels' per-problem part of the guard)
+__device__ __forceinline__ int scale_in_range(double l, double tr) {
+    return fast_range_ok(l) & (int)(l > 0.0) & (int)(tr > 0.0) & (int)(tr <= 0x1p64);
+}
+
 // t3 follows NumPy pairwise_sum streamed over k (no product array): 0 + e0 + ... for d < 8;
 // 8 partial sums for 8 <= d <= 128.  (d > 128 rejected at the ABI.)
 
@@ -209,6 +269,22 @@ __device__ __forceinline__ double diag_value_ct(const double (&gi)[D], double tr
     }
     // finish_pair(0, 0, 0, t3s): t1 = -0/1, t2 = tr/1, t3 = t3s/1 -> (-0 + tr) + t3s
     return finish_pair(0.0, 0.0, 0.0, t3s, tr);
+}
+
+// The d <= 8 kernels' per-pair rule: the compact arithmetic when cok (l, tr and both rows in range,
+// see pair_compact_ct), the exact one otherwise.  A real branch (not compute-both-and-select).
+template <int D>
+__device__ __forceinline__ double pair_value_sel(bool cok, const double (&xi)[D], const double (&gi)[D],
+                                                 const double* xj, const double* gj, double l, double l2,
+                                                 double m3l2, double tr) {
+    if (cok) return pair_compact_ct<D>(xi, gi, xj, gj, l, m3l2, tr);
+    return pair_value_ct<D>(xi, gi, xj, gj, l, l2, tr);
+}
+
+template <int D>
+__device__ __forceinline__ double diag_value_sel(bool cok, const double (&gi)[D], double tr) {
+    if (cok) return diag_compact_ct<D>(gi, tr);
+    return diag_value_ct<D>(gi, tr);
 }
 
 // Runtime d (1..128): point a strided by sa (SoA column: sa = ld), point b strided by sb.

@@ -122,8 +122,32 @@ def lib() -> ctypes.CDLL:
                 import torch  # noqa: F401  -- map torch's HIP runtime before ours resolves against it
                 # ST_HIP_LIB: another build of the same ABI (same-box A/B timing of a kernel change,
                 # scripts/ab_run.sh); the in-tree library otherwise
-                _LIB = load_library(os.environ.get('ST_HIP_LIB') or LIB_PATH)
+                L = load_library(os.environ.get('ST_HIP_LIB') or LIB_PATH)
+                mode = os.environ.get('ST_ARITH')
+                if mode:
+                    if mode not in ARITHMETIC:
+                        raise ValueError(f'ST_ARITH={mode!r}: expected one of {sorted(ARITHMETIC)}')
+                    L.st_tune(11, ARITHMETIC[mode])
+                _LIB = L
     return _LIB
+
+
+# greedy-kernel arithmetic (st_tune key 11; include/stein_thinning_hip.h)
+ARITHMETIC = {'exact': 0, 'compact': 1}
+
+
+def set_arithmetic(mode: str) -> None:
+    """Arithmetic of the d <= 8 greedy kernels (thin / thin_gf / _greedy_search on a Stein integrand).
+
+    'compact' (default): the IMQ Stein-kernel value regrouped around one correctly rounded reciprocal
+    square root -- a few ulps from NumPy's evaluation of vfk0_imq, ~2.3x fewer fp64 instructions per
+    pair; selections equal the reference's on every fixture it holds (tests/test_oracle_compact.py).
+    'exact': NumPy's evaluation order, rounding for rounding (correctly rounded powers).  Pairs with a
+    coordinate outside [2^-60, 2^60] always take the exact arithmetic.  Process-wide; every rank of a
+    sharded run must use the same mode (ST_ARITH in the environment sets it at library load)."""
+    if mode not in ARITHMETIC:
+        raise ValueError(f'arithmetic {mode!r}: expected one of {sorted(ARITHMETIC)}')
+    check(lib().st_tune(11, ARITHMETIC[mode]), 'set_arithmetic')
 
 
 def check_host(rc: int, what: str = '') -> None:

@@ -65,7 +65,11 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * record pitch in bytes (power of two, 16..4096; -1 = automatic = 256 with one replica, 16 with
  * several, narrowed to what the workspace holds), key 10 = persistent kernel record replicas
  * (power of two, 1..32: every block stores its per-step record into each replica and block b
- * sweeps replica b % replicas; -1 = automatic).
+ * sweeps replica b % replicas; -1 = automatic), key 11 = arithmetic of the d <= 8 greedy kernels
+ * (1 = compact, the default: the kernel value regrouped around one reciprocal square root, a few
+ * ulps from NumPy's evaluation, for every pair whose two rows and l, tr lie in [2^-60, 2^60];
+ * 0 = exact: NumPy's evaluation order rounding for rounding; other pairs are always exact -- see
+ * oracle/stein_ref.c and DESIGN.md §3; all ranks of a sharded run must use the same value).
  */
 int st_tune(int32_t key, int32_t value);
 

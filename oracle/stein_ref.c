@@ -23,6 +23,18 @@
  * Greedy: A = diag; idx0 = argmin A; A = fl(A + 2*col); first minimum, NaN counts as minimum
  * (np.argmin) -- JAX_Stein_Thinning.ipynb cell 22 (~281-295), report.tex:413-426.
  *
+ * Compact arithmetic (arith = 1; the kernels' default for d <= 8 since round 3): the same kernel value
+ * by the shortest exact-enough route -- with S = SEQ_FMA_k delta_k^2, G = SEQ_FMA_k (sa_k - sb_k) delta_k,
+ * P = SEQ_FMA_k sa_k sb_k (first term a product, then one fma per coordinate):
+ *   qf = fma(l, S, 1)   y = RN(1 / RN(sqrt(qf)))   T1 = fl(-3 l^2) S   T2 = fma(l, G, tr)
+ *   k  = y * fma(y^2, fma(y^2, T1, T2), P)            (= t1 + t2 + t3 of the reference, regrouped)
+ * a few ulps from the NumPy evaluation instead of bit-identical to it; it applies to a pair (d <= 8)
+ * only when every coordinate of both rows (x and g) is 0 or of magnitude in [2^-60, 2^60], l is in
+ * [2^-60, 2^60] and 0 < tr <= 2^64 (no intermediate can overflow, underflow or be NaN); other pairs
+ * take the exact arithmetic (pair_any: a per-pair rule, independent of any row partition).  Index
+ * parity with the reference then rests on argmin margins (tests/golden/config*_numpy_indices.json:
+ * >= 1.2e9 ulps), like the NumPy path's own 1-ulp pow differences across CPUs.
+ *
  * Build: gcc -O2 -fPIC -shared -ffp-contract=off -pthread -o oracle/_build/libstein_ref.so oracle/stein_ref.c -lm
  */
 #include <math.h>
@@ -95,6 +107,56 @@ static double pair_value(const double *a, int64_t sa_stride, const double *b, in
     return (t1 + t2) + t3;
 }
 
+/* compact arithmetic (header); y2 = y*y, m3l2 = fl(-3 * fl(l*l)) */
+static double pair_compact(const double *a, int64_t sa_stride, const double *b, int64_t sb_stride,
+                           const double *ga, const double *gb, int d, double l, double tr) {
+    double S = 0, G = 0, P = 0;
+    for (int k = 0; k < d; k++) {
+        double dl = a[k * sa_stride] - b[k * sb_stride];
+        double gd = ga[k * sa_stride] - gb[k * sb_stride];
+        double pa = ga[k * sa_stride], pb = gb[k * sb_stride];
+        if (k == 0) { S = dl * dl; G = gd * dl; P = pa * pb; }
+        else { S = fma(dl, dl, S); G = fma(gd, dl, G); P = fma(pa, pb, P); }
+    }
+    double m3l2 = -3.0 * (l * l);
+    double q = fma(l, S, 1.0);
+    double y = 1.0 / sqrt(q);
+    double y2 = y * y;
+    double in = fma(y2, m3l2 * S, fma(l, G, tr));
+    return y * fma(y2, in, P);
+}
+
+static int in_range(double v) {
+    double a = fabs(v);
+    return a == 0.0 || (a >= 0x1p-60 && a <= 0x1p60);
+}
+
+static int scale_ok(double l, double tr) { return in_range(l) && l > 0.0 && tr > 0.0 && tr <= 0x1p64; }
+
+static int row_ok(const double *x, const double *g, int64_t stride, int d) {
+    for (int k = 0; k < d; k++)
+        if (!in_range(x[k * stride]) || !in_range(g[k * stride])) return 0;
+    return 1;
+}
+
+/* the kernels' per-pair rule (stein_math.hpp pair_value_sel): compact arithmetic when arith = 1,
+ * d <= 8, l and tr in range and both rows in range; the exact arithmetic otherwise */
+static double pair_any(int arith, const double *a, int64_t sa_stride, const double *b, int64_t sb_stride,
+                       const double *ga, const double *gb, int d, double l, double tr) {
+    if (arith == 1 && d <= 8 && scale_ok(l, tr) && row_ok(a, ga, sa_stride, d) && row_ok(b, gb, sb_stride, d))
+        return pair_compact(a, sa_stride, b, sb_stride, ga, gb, d, l, tr);
+    return pair_value(a, sa_stride, b, sb_stride, ga, gb, d, l, tr);
+}
+
+/* 1 if every pair of the problem takes the compact arithmetic (tests) */
+int sr_compact_ok(const double *x, const double *g, int64_t n, int d, double l, double tr) {
+    if (d > 8 || !scale_ok(l, tr)) return 0;
+    for (int64_t i = 0; i < n; i++)
+        if (!row_ok(x + i * d, g + i * d, 1, d)) return 0;
+    return 1;
+}
+
+/* running-sum update: fl(A + 2k) (2k exact); the kernels' fma(2, k, A) is the same bits */
 static int better(double a, int64_t ia, double b, int64_t ib) {
     if (isnan(a)) return isnan(b) ? (ia < ib) : 1;
     if (isnan(b)) return 0;
@@ -106,10 +168,10 @@ static int better(double a, int64_t ia, double b, int64_t ib) {
  * Returns 0 on success, -1 on unsupported d.
  */
 int sr_greedy(const double *x, const double *g, const double *w, int64_t n, int d,
-              double l, double tr, int64_t m, uint32_t *idx, double *A) {
+              double l, double tr, int64_t m, uint32_t *idx, double *A, int arith) {
     if (d < 1 || d > 128) return -1;
     for (int64_t i = 0; i < n; i++) {
-        double k = pair_value(x + i * d, 1, x + i * d, 1, g + i * d, g + i * d, d, l, tr);
+        double k = pair_any(arith, x + i * d, 1, x + i * d, 1, g + i * d, g + i * d, d, l, tr);
         if (w) k = (k * w[i]) * w[i];
         A[i] = k;
     }
@@ -117,7 +179,7 @@ int sr_greedy(const double *x, const double *g, const double *w, int64_t n, int 
         if (t > 0) {
             int64_t j = idx[t - 1];
             for (int64_t i = 0; i < n; i++) {
-                double k = pair_value(x + i * d, 1, x + j * d, 1, g + i * d, g + j * d, d, l, tr);
+                double k = pair_any(arith, x + i * d, 1, x + j * d, 1, g + i * d, g + j * d, d, l, tr);
                 if (w) k = (k * w[i]) * w[j];
                 A[i] = A[i] + 2.0 * k;
             }
@@ -145,6 +207,7 @@ typedef struct {
     int64_t n, m;
     int d, nthreads;
     double l, tr;
+    int arith;
     uint32_t *idx;
     double *A;
     double *bv;
@@ -161,7 +224,7 @@ static void *mt_worker(void *p) {
     const int64_t r0 = c->n * a->tid / c->nthreads, r1 = c->n * (a->tid + 1) / c->nthreads;
     for (int64_t i = r0; i < r1; i++) {
         const double *xi = c->x + i * d, *gi = c->g + i * d;
-        double k = pair_value(xi, 1, xi, 1, gi, gi, d, c->l, c->tr);
+        double k = pair_any(c->arith, xi, 1, xi, 1, gi, gi, d, c->l, c->tr);
         if (c->w) k = (k * c->w[i]) * c->w[i];
         c->A[i] = k;
     }
@@ -170,7 +233,7 @@ static void *mt_worker(void *p) {
             int64_t j = c->idx[t - 1];
             const double *xj = c->x + j * d, *gj = c->g + j * d;
             for (int64_t i = r0; i < r1; i++) {
-                double k = pair_value(c->x + i * d, 1, xj, 1, c->g + i * d, gj, d, c->l, c->tr);
+                double k = pair_any(c->arith, c->x + i * d, 1, xj, 1, c->g + i * d, gj, d, c->l, c->tr);
                 if (c->w) k = (k * c->w[i]) * c->w[j];
                 c->A[i] = c->A[i] + 2.0 * k;
             }
@@ -196,12 +259,12 @@ static void *mt_worker(void *p) {
 }
 
 int sr_greedy_mt(const double *x, const double *g, const double *w, int64_t n, int d,
-                 double l, double tr, int64_t m, uint32_t *idx, double *A, int nthreads) {
+                 double l, double tr, int64_t m, uint32_t *idx, double *A, int nthreads, int arith) {
     if (d < 1 || d > 128 || n < 1) return -1;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     if (nthreads > n) nthreads = (int)n;
-    mt_ctx c = {x, g, w, n, m, d, nthreads, l, tr, idx, A, NULL, NULL};
+    mt_ctx c = {x, g, w, n, m, d, nthreads, l, tr, arith, idx, A, NULL, NULL};
     c.bv = (double *)malloc(sizeof(double) * nthreads);
     c.bi = (int64_t *)malloc(sizeof(int64_t) * nthreads);
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
@@ -244,12 +307,12 @@ void sr_pow_15_25(const double *q, int64_t n, double *p15, double *p25) {
 
 /* pair values out[p] = k(i1[p], i2[p]) with weights fl(fl(k*w_i1)*w_i2) */
 int sr_pairs(const double *x, const double *g, const double *w, int64_t n, int d, double l, double tr,
-             const int64_t *i1, const int64_t *i2, int64_t L, double *out) {
-    (void)n;
+             const int64_t *i1, const int64_t *i2, int64_t L, double *out, int arith) {
     if (d < 1 || d > 128) return -1;
+    (void)n;
     for (int64_t p = 0; p < L; p++) {
         int64_t a = i1[p], b = i2[p];
-        double k = pair_value(x + a * d, 1, x + b * d, 1, g + a * d, g + b * d, d, l, tr);
+        double k = pair_any(arith, x + a * d, 1, x + b * d, 1, g + a * d, g + b * d, d, l, tr);
         if (w) k = (k * w[a]) * w[b];
         out[p] = k;
     }

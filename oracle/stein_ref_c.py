@@ -24,23 +24,37 @@ def lib():
         L = ctypes.CDLL(LIB)
         dp, i64 = ctypes.c_void_p, ctypes.c_int64
         L.sr_greedy.restype = ctypes.c_int
-        L.sr_greedy.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp]
+        L.sr_greedy.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp,
+                                ctypes.c_int]
         L.sr_greedy_mt.restype = ctypes.c_int
         L.sr_greedy_mt.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp,
-                                   ctypes.c_int]
+                                   ctypes.c_int, ctypes.c_int]
         L.sr_pow_15_25.restype = None
         L.sr_pow_15_25.argtypes = [dp, i64, dp, dp]
         L.sr_pairs.restype = ctypes.c_int
-        L.sr_pairs.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, dp, i64, dp]
+        L.sr_pairs.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, dp, dp, i64, dp,
+                               ctypes.c_int]
+        L.sr_compact_ok.restype = ctypes.c_int
+        L.sr_compact_ok.argtypes = [dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double]
         _lib = L
     return _lib
+
+
+# arithmetic of the kernels' bit model: 'exact' = NumPy's evaluation order rounding for rounding,
+# 'compact' = the regrouped form (stein_ref.c header) the d <= 8 kernels use by default
+ARITH = {'exact': 0, 'compact': 1}
+DEFAULT_ARITH = 'compact'
+
+
+def _a(arith):
+    return ARITH[arith or DEFAULT_ARITH]
 
 
 def _p(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
-def greedy(x, g, w, l, tr, m):
+def greedy(x, g, w, l, tr, m, arith=None):
     """Bit-model greedy run: returns (idx uint32, running sums A)."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     g = np.ascontiguousarray(g, dtype=np.float64)
@@ -48,7 +62,7 @@ def greedy(x, g, w, l, tr, m):
     n, d = x.shape
     idx = np.empty(m, dtype=np.uint32)
     A = np.empty(n, dtype=np.float64)
-    rc = lib().sr_greedy(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A))
+    rc = lib().sr_greedy(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A), _a(arith))
     assert rc == 0
     return idx, A
 
@@ -59,7 +73,7 @@ def host_threads():
     return max(1, min(int(os.environ.get('OMP_NUM_THREADS', 0)) or (os.cpu_count() or 1), 16))
 
 
-def greedy_mt(x, g, w, l, tr, m, nthreads=None):
+def greedy_mt(x, g, w, l, tr, m, nthreads=None, arith=None):
     """sr_greedy over row blocks on host threads: same indices and bit-identical A as greedy()."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     g = np.ascontiguousarray(g, dtype=np.float64)
@@ -67,21 +81,29 @@ def greedy_mt(x, g, w, l, tr, m, nthreads=None):
     n, d = x.shape
     idx = np.empty(m, dtype=np.uint32)
     A = np.empty(n, dtype=np.float64)
-    rc = lib().sr_greedy_mt(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A), nthreads or host_threads())
+    rc = lib().sr_greedy_mt(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A), nthreads or host_threads(),
+                            _a(arith))
     assert rc == 0
     return idx, A
 
 
-def pairs(x, g, w, l, tr, i1, i2):
+def pairs(x, g, w, l, tr, i1, i2, arith=None):
     x = np.ascontiguousarray(x, dtype=np.float64)
     g = np.ascontiguousarray(g, dtype=np.float64)
     w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
     i1 = np.ascontiguousarray(i1, dtype=np.int64)
     i2 = np.ascontiguousarray(i2, dtype=np.int64)
     out = np.empty(i1.shape[0], dtype=np.float64)
-    rc = lib().sr_pairs(_p(x), _p(g), _p(w), x.shape[0], x.shape[1], l, tr, _p(i1), _p(i2), i1.shape[0], _p(out))
+    rc = lib().sr_pairs(_p(x), _p(g), _p(w), x.shape[0], x.shape[1], l, tr, _p(i1), _p(i2), i1.shape[0], _p(out), _a(arith))
     assert rc == 0
     return out
+
+
+def compact_ok(x, g, l, tr):
+    """1 if the compact arithmetic applies (every coordinate 0 or in [2^-60, 2^60], l and tr in range)."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    g = np.ascontiguousarray(g, dtype=np.float64)
+    return bool(lib().sr_compact_ok(_p(x), _p(g), x.shape[0], x.shape[1], l, tr))
 
 
 def pow_15_25(q):

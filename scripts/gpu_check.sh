@@ -22,6 +22,13 @@ if [[ $MODE == all || $MODE == test ]]; then
   step smoke 300 python -c "import __graft_entry__ as g; g.smoke()"
   step pytest_gpu 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread
 fi
+if [[ $MODE == ab ]]; then   # same-box A/B of the persistent kernel (scripts/build_ab.sh first)
+  step ab 900 bash scripts/ab_run.sh
+fi
+if [[ $MODE == files ]]; then   # gpu_check.sh files <pytest args...>
+  shift
+  step pytest_files 1100 python -u -m pytest -m gpu -x -q --timeout 300 --timeout-method thread "$@"
+fi
 if [[ $MODE == all || $MODE == bench ]]; then
   step bench 900 python bench.py --steps 3 --warmup 1
 fi

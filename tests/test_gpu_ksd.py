@@ -93,8 +93,8 @@ def test_large_n_against_c_bit_model_pairs():
     tot = 0.0
     for i in cols:
         a = np.arange(i)
-        tot += 2.0 * np.sum(oracle_c.pairs(s, gs, None, linv, dev.linv_trace, np.full(i, i), a))
-    diag = oracle_c.pairs(s, gs, None, linv, dev.linv_trace, cols, cols)
+        tot += 2.0 * np.sum(oracle_c.pairs(s, gs, None, linv, dev.linv_trace, np.full(i, i), a, arith='exact'))
+    diag = oracle_c.pairs(s, gs, None, linv, dev.linv_trace, cols, cols, arith='exact')
     tail = tot + np.sum(diag)
     S = (ks[-1] * n) ** 2 - (ks[n - 201] * (n - 200)) ** 2
     np.testing.assert_allclose(S, tail, rtol=1e-9)

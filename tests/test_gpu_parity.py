@@ -4,6 +4,7 @@ Bar: selected indices identical to the NumPy oracle (itself pinned to the refere
 outputs); running sums / pair values bit-identical to the C bit model (oracle/stein_ref.c); KSD within
 1e-10 relative of the NumPy oracle (north_star tolerance 1e-6).
 """
+import contextlib
 import warnings
 
 import numpy as np
@@ -24,6 +25,18 @@ from stein_thinning import stein as ss  # noqa: E402
 from stein_thinning import thinning as st  # noqa: E402
 from stein_thinning.device import DeviceProblem  # noqa: E402
 from stein_thinning.distributed import HipShardBackend, shard_bounds  # noqa: E402
+
+
+@contextlib.contextmanager
+def arith(mode):
+    """st_tune key 11 for the block: the greedy kernels' arithmetic ('compact' = the default)."""
+    from stein_thinning import _native
+    L = _native.lib()
+    assert L.st_tune(11, {'exact': 0, 'compact': 1}[mode]) == 0
+    try:
+        yield
+    finally:
+        L.st_tune(11, -1)
 
 
 def _native_loaded():
@@ -125,9 +138,10 @@ def _rw_chain(n, d, seed, dup_every=3):
     return x, g
 
 
+@pytest.mark.parametrize('mode', ['compact', 'exact'])
 @pytest.mark.parametrize('d', [1, 2, 3, 4, 5, 7, 8, 9, 16, 50])
 @pytest.mark.parametrize('gf', [False, True])
-def test_running_sums_bit_exact_vs_c_model(d, gf):
+def test_running_sums_bit_exact_vs_c_model(d, gf, mode):
     n, m = 4099, 25      # odd n: exercises the padded lane pair
     x, g = _rw_chain(n, d, seed=d)
     s, gs = o._validate_and_standardize(x, g, True)
@@ -138,8 +152,9 @@ def test_running_sums_bit_exact_vs_c_model(d, gf):
         lw = -0.1 * np.sum(x * x, axis=1)
         w = np.exp(lw - lw.min())
     prob = DeviceProblem(s, gs, w, l, tr)
-    idx, A = prob.greedy(m, return_sums=True)
-    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    with arith(mode):
+        idx, A = prob.greedy(m, return_sums=True)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m, arith=mode)
     np.testing.assert_array_equal(idx, cidx)
     assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
 
@@ -244,11 +259,15 @@ def test_wide_persistent_d50_bit_exact(n, gf):
     assert np.array_equal(sA, A)
 
 
+@pytest.mark.parametrize('mode', ['compact', 'exact'])
+@pytest.mark.parametrize('steps', [False, True])
 @pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
-def test_persistent_exact_path_outside_fast_range(d, gf):
+def test_persistent_exact_path_outside_fast_range(d, gf, steps, mode):
     """Rows with components outside [2^-60, 2^60] (tiny / huge scores, tiny coordinates) force the
     persistent kernel's general arithmetic for their blocks and for steps whose selected row is
-    out of range (csrc/stein_math.hpp fast_range_ok); results stay bit-identical to the C model."""
+    out of range (csrc/stein_math.hpp fast_range_ok) -- with the compact arithmetic, the per-pair
+    rule (compact iff both rows in range: the mixed sweep); results stay bit-identical to the C
+    model, on the persistent kernel and on the launch-per-step kernels (steps)."""
     n, m = 200_003, 40
     x, g = _rw_chain(n, d, seed=7 + d)
     s, gs = o._validate_and_standardize(x, g, True)
@@ -267,8 +286,15 @@ def test_persistent_exact_path_outside_fast_range(d, gf):
     if gf:
         lw = -0.2 * np.sum(x * x, axis=1)
         w = np.exp(lw - lw.min())
-    idx, A = DeviceProblem(s, gs, w, l, tr).greedy(m, return_sums=True)
-    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    from stein_thinning import _native
+    if steps:
+        _native.lib().st_tune(3, 0)
+    try:
+        with arith(mode):
+            idx, A = DeviceProblem(s, gs, w, l, tr).greedy(m, return_sums=True)
+    finally:
+        _native.lib().st_tune(3, -1)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m, arith=mode)
     np.testing.assert_array_equal(idx, cidx)
     assert np.array_equal(A, cA), np.flatnonzero(A != cA)[:10]
     if not gf:   # Langevin: the tiny-score rows have the smallest diagonal and are selected
@@ -286,11 +312,12 @@ def test_pair_values_bit_exact_vs_c_model(d):
     i1 = rng.integers(0, 700, size=5000)
     i2 = rng.integers(0, 700, size=5000)
     got = integ(i1, i2)
-    want = oracle_c.pairs(s, gs, w, integ.linv_scale, integ.linv_trace, i1, i2)
+    # the integrand protocol (vfk0_imq values) keeps the exact arithmetic
+    want = oracle_c.pairs(s, gs, w, integ.linv_scale, integ.linv_trace, i1, i2, arith='exact')
     assert np.array_equal(got, want)
     # integrand protocol forms used by the reference: (slice, slice), (slice, [j])
     np.testing.assert_array_equal(integ(slice(None), [5]), oracle_c.pairs(
-        s, gs, w, integ.linv_scale, integ.linv_trace, np.arange(700), np.full(700, 5)))
+        s, gs, w, integ.linv_scale, integ.linv_trace, np.arange(700), np.full(700, 5), arith='exact'))
     # and against the NumPy oracle integrand (different pow rounding: <= 1e-15 relative)
     ref = o._make_stein_gf_integrand(x, np.zeros(700), lw, g, preconditioner='med')
     np.testing.assert_allclose(integ(slice(None), slice(None)), ref(slice(None), slice(None)), rtol=1e-14)

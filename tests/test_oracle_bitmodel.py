@@ -89,7 +89,7 @@ def test_c_model_is_scalar_model_with_correct_rounding(d):
     l, tr = linv[0, 0], np.trace(linv)
     i1 = np.arange(60)
     i2 = np.full(60, 5)
-    got = oracle_c.pairs(x, g, None, l, tr, i1, i2)
+    got = oracle_c.pairs(x, g, None, l, tr, i1, i2, arith='exact')
     want = np.array([_model(x[i], x[5], g[i], g[5], l, tr, _cr_pow) for i in i1])
     np.testing.assert_array_equal(got, want)
 
@@ -181,12 +181,15 @@ def _config_inputs(x, g, log_p=None, log_q=None):
     return s, gs, w, float(linv[0, 0]), float(np.trace(linv))
 
 
-def test_bitmodel_config4_full_length_equals_numpy_fixture():
+@pytest.mark.parametrize('mode', ['compact', 'exact'])
+def test_bitmodel_config4_full_length_equals_numpy_fixture(mode):
+    """Both arithmetics of the d <= 8 kernels select all 1 000 indices of the NumPy fixture."""
     from bench import lv_surrogate
     fx = _golden_config('config4_numpy_indices.json')
     x, g, _, _ = lv_surrogate(2_000_000, 12345)
     s, gs, _, l, tr = _config_inputs(x, g)
-    idx, _ = oracle_c.greedy_mt(s, gs, None, l, tr, 1000)
+    assert oracle_c.compact_ok(s, gs, l, tr)
+    idx, _ = oracle_c.greedy_mt(s, gs, None, l, tr, 1000, arith=mode)
     np.testing.assert_array_equal(idx, fx['indices'])
     assert fx['min_margin_ulps'] > 1e3   # no step is a near tie that 1-ulp pow differences could flip
 
