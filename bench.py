@@ -134,7 +134,7 @@ def make_integrand(cfg):
     return st._make_stein_integrand(x, g, preconditioner='med'), x, g
 
 
-def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None):
+def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None, arith='compact'):
     """Host baselines on the same standardised input (test-infrastructure code, timed only):
     * primary: the C restatement (oracle/stein_ref.c sr_greedy_mt -- the kernels' bit model, rows
       split over host threads like the reference's process fan-out, code/src/utils/parallel.py:48-52)
@@ -147,7 +147,7 @@ def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None):
     s, g, w = integrand.sample, integrand.gradient, integrand.weights
     nt = stein_ref_c.host_threads()
     t0 = time.perf_counter()
-    cidx, _ = stein_ref_c.greedy_mt(s, g, w, integrand.linv_scale, integrand.linv_trace, cfg['m'], nt)
+    cidx, _ = stein_ref_c.greedy_mt(s, g, w, integrand.linv_scale, integrand.linv_trace, cfg['m'], nt, arith=arith)
     dt_c = time.perf_counter() - t0
     vfk0 = ref.make_imq(s, 'med')
     if w is None:
@@ -164,7 +164,8 @@ def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None):
     host = f"{platform.processor() or platform.machine()} ({os.cpu_count()} logical CPUs visible)"
     return {'value': full / dt_c, 'unit': 'pair-evals/s', 'cores': nt, 'kind': 'port',
             'sample': (f"oracle/stein_ref.c sr_greedy_mt (C restatement of the reference greedy loop, "
-                       f"JAX_Stein_Thinning.ipynb:281-295, bit model of the kernels) on {nt} host threads: the full "
+                       f"JAX_Stein_Thinning.ipynb:281-295, bit model of the kernels, {arith} arithmetic) on {nt} host "
+                       f"threads: the full "
                        f"n={cfg['n']}, m={cfg['m']} thin ({full:.3g} pair-evals) in {dt_c:.1f} s; host {host}"),
             'same_indices_as_gpu': None if gpu_idx is None else bool(np.array_equal(cidx, gpu_idx)),
             'numpy_1core': {'value': pairs / dt, 'unit': 'pair-evals/s', 'cores': 1,
@@ -288,6 +289,8 @@ def main():
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
     ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
     ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
+    ap.add_argument('--arith', default='compact', choices=['compact', 'exact'],
+                    help='arithmetic of the d <= 8 greedy kernels (stein_thinning.set_arithmetic)')
     ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
                          '(row-sharded, RCCL all-reduce of the n-length column-sum vector); ranks: launcher '
@@ -326,6 +329,9 @@ def main():
     n, m = cfg['n'], cfg['m']
     integrand, host_x, host_g = make_integrand(cfg)
     d = integrand.sample.shape[1]
+    import stein_thinning
+    stein_thinning.set_arithmetic(args.arith)
+    arithmetic = args.arith
 
     if not sharded:
         prob = integrand.device_problem()
@@ -375,12 +381,18 @@ def main():
         bytes_per_pair = 16 * d + (24 if gf else 16)
         # algorithmic work per pair: what `frac` is priced on
         flop_per_pair = algorithmic_flop_per_pair(d, gf)
-        # what the persistent kernel's hot loop actually issues, counted in its ISA
-        # (greedy_persistent<4,false,8,512>; tools/pair_rate.hip): 40 v_mul_f64 + 28 v_add_f64 + 31
-        # v_fma/v_fmac_f64 + 1 v_rsq_f64 + 1 v_cmp_f64 = 101 fp64 VALU instructions, 130 flop (fma = 2);
-        # each further coordinate adds 13; the gradient-free weights add 2 mul
-        instr_per_pair = 101 + 13 * (d - 4) + (2 if gf else 0)
-        issue_flop_per_pair = 130 + 13 * (d - 4) + (2 if gf else 0)
+        # what the persistent kernel's hot loop actually issues, counted in its ISA.  Compact
+        # arithmetic (the default, stein_math.hpp pair_compact_ct): 8 v_mul_f64 + 9 v_add_f64 + 25
+        # v_fma/v_fmac_f64 (running-sum update included) + 1 v_rsq_f64 + 1 v_cmp_f64 = 44 fp64 VALU
+        # instructions, 67 flop (fma = 2); each further coordinate adds 5 (2 sub + 3 fma, 8 flop).
+        # Exact arithmetic (ST_ARITH=exact): 40 mul + 28 add + 31 fma + 1 rsq + 1 cmp = 101, 130 flop;
+        # each further coordinate adds 13.  The gradient-free weights add 2 mul.
+        if arithmetic == 'compact' and d <= 8:
+            instr_per_pair = 44 + 5 * (d - 4) + (2 if gf else 0)
+            issue_flop_per_pair = 67 + 8 * (d - 4) + (2 if gf else 0)
+        else:
+            instr_per_pair = 101 + 13 * (d - 4) + (2 if gf else 0)
+            issue_flop_per_pair = 130 + 13 * (d - 4) + (2 if gf else 0)
         pmc = os.path.join(ROOT, 'profiles', 'pmc_traffic.json')
         pmc_rec = json.load(open(pmc)) if os.path.exists(pmc) else {}
         if persistent:
@@ -441,7 +453,7 @@ def main():
                             'bytes_per_pair': bytes_per_pair,
                             'timing': 'HIP events around back-to-back single-step launches'}
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(cfg, integrand, args.cpu_steps, result_idx)
+            cpu = cpu_baseline(cfg, integrand, args.cpu_steps, result_idx, arithmetic)
         e2e = None
         if world == 1 and not cfg['gf'] and not cfg.get('d50'):
             # the drop-in call on host arrays (not `value`): standardisation + 'med' + H2D upload +
@@ -485,6 +497,7 @@ def main():
                        'preconditioner': 'med', 'kernel': 'gradient-free' if integrand.weights is not None else 'langevin',
                        'parallelism': (f'rows-sharded x{world}, per-step exchange: {runner.mode}'
                                        if sharded else 'single-gpu'),
+                       'arithmetic': arithmetic if d <= 8 else 'exact',
                        'wallclock_thin_s': elapsed / args.steps,
                        'first_indices': result_idx[:8].tolist()},
             'exchange': exchange,

@@ -90,9 +90,10 @@ __global__ __launch_bounds__(256) void kmat_kernel(PairArgs p, int64_t k, double
 // run computes csum over its rows and all-reduces the n-length vector (RCCL) before ksd_finish.
 // One thread per column i (its row in registers); rows a staged kRows at a time in LDS and read
 // as block-uniform broadcasts; 4 blocks (16 waves) per CU; block b takes column block NB-1-b so
-// the heavy (late) columns are dispatched first.  Per pair: the bits of pair_value_ct (the
-// range-guarded fast arithmetic when the block's columns and the staged rows admit it); per
-// column: a sequential sum in increasing a.
+// the heavy (late) columns are dispatched first.  Per pair: the compact arithmetic (st_tune key 11,
+// the default; stein_math.hpp pair_compact_ct) when the block's columns and the staged rows are all
+// in range, else the bits of pair_value_ct (the range-guarded fast form when they admit it: the
+// exact setting); per column: a sequential sum in increasing a.
 // ------------------------------------------------------------------------------------------
 constexpr int kColBlock = 256;
 constexpr int kColsumUnroll = 2;   // rows per iteration of the column-sum sweep
@@ -105,6 +106,7 @@ struct ColsumArgs {
     double l, tr;
     int64_t a0, a1;
     double* csum;
+    int compact;
 };
 
 template <int D, bool GF>
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
         cok &= fast_range_ok(xi[k]) & fast_range_ok(gi[k]);
     }
     const double wi = (GF && live) ? p.w[i] : 1.0;
-    const double l = p.l, l2 = p.l * p.l, tr = p.tr;
+    const double l = p.l, l2 = p.l * p.l, m3l2 = -3.0 * l2, tr = p.tr;
     const int col_fast = __syncthreads_and(cok);
     const int64_t a_stop = p.a1 < c0 + R ? p.a1 : c0 + R;   // rows a < i <= c0 + R - 1
     double acc = 0.0;
@@ -151,14 +153,18 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
         // every row of a tile that ends at or before the block's first column precedes all its
         // columns: no per-pair triangle predicate (only the diagonal tile keeps it)
         const bool below = ac + cnt <= c0;
-        auto sweep = [&](auto fast_tag, auto below_tag) {
-            constexpr bool FAST = decltype(fast_tag)::value, BELOW = decltype(below_tag)::value;
+        // AR: 0 exact general, 1 exact range-guarded (same bits), 2 compact
+        auto sweep = [&](auto ar_tag, auto below_tag) {
+            constexpr int AR = decltype(ar_tag)::value;
+            constexpr bool BELOW = decltype(below_tag)::value;
             asm volatile(";; colsum variant" ::);
             auto pair_at = [&](int e) -> double {
                 double xa[D], ga[D];
 #pragma unroll
                 for (int k = 0; k < D; ++k) { xa[k] = sx[k][e]; ga[k] = sg[k][e]; }
-                double kv = pair_value_ct<D, FAST>(xi, gi, xa, ga, l, l2, tr);
+                double kv;
+                if constexpr (AR == 2) kv = pair_compact_ct<D>(xi, gi, xa, ga, l, m3l2, tr);
+                else kv = pair_value_ct<D, AR == 1>(xi, gi, xa, ga, l, l2, tr);
                 if constexpr (GF) kv = (kv * wi) * sw[e];
                 return kv;
             };
@@ -181,12 +187,18 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
                 else acc = (ac + e < i) ? acc + kv : acc;
             }
         };
-        if (fast) {
-            if (below) sweep(std::true_type{}, std::true_type{});
-            else sweep(std::true_type{}, std::false_type{});
+        using C0 = std::integral_constant<int, 0>;
+        using C1 = std::integral_constant<int, 1>;
+        using C2 = std::integral_constant<int, 2>;
+        if (fast && p.compact) {
+            if (below) sweep(C2{}, std::true_type{});
+            else sweep(C2{}, std::false_type{});
+        } else if (fast) {
+            if (below) sweep(C1{}, std::true_type{});
+            else sweep(C1{}, std::false_type{});
         } else {
-            if (below) sweep(std::false_type{}, std::true_type{});
-            else sweep(std::false_type{}, std::false_type{});
+            if (below) sweep(C0{}, std::true_type{});
+            else sweep(C0{}, std::false_type{});
         }
     }
     if (live) p.csum[i] = acc;
@@ -445,7 +457,7 @@ static void launch_colsum_ct(const ColsumArgs& a, unsigned grid, hipStream_t s) 
 
 hipError_t launch_ksd_colsum(const PairArgs& p, int64_t n, int64_t a0, int64_t a1, double* csum,
                              hipStream_t s) {
-    ColsumArgs a{p.x, p.g, p.w, n, p.ld, p.l, p.tr, a0, a1, csum};
+    ColsumArgs a{p.x, p.g, p.w, n, p.ld, p.l, p.tr, a0, a1, csum, arith_compact()};
     // columns at or below a0 get no rows: zero them, then launch only the blocks above a0
     const int64_t first_block = (a0 + 1) / kColBlock;          // block containing column a0 + 1
     const int64_t nb = (n + kColBlock - 1) / kColBlock;

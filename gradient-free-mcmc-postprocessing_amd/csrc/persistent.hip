@@ -97,6 +97,13 @@ __device__ __forceinline__ void scan_take_idx(double a, uint32_t ia, double& b, 
     ib = take ? ia : ib;
 }
 
+// one f64 through a buffer descriptor: byte offsets voff (per lane) + soff (uniform, an SGPR)
+__device__ __forceinline__ double buf_load_f64(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+    const u32x2 v = __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0);
+    return __longlong_as_double((long long)(((uint64_t)v.y << 32) | v.x));
+}
+
 // value known to be identical in every lane: move it to SGPRs
 __device__ __forceinline__ double uniform(double v) {
     const uint64_t b = (uint64_t)__double_as_longlong(v);
@@ -628,10 +635,13 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     extern __shared__ __attribute__((aligned(16))) double lds[];
     Scratch* sc = reinterpret_cast<Scratch*>(lds);
     const int RL = a.RL;
-    double* sx = lds + (sizeof(Scratch) + 15) / 16 * 2;   // [D][RL]
-    double* sg = sx + (int64_t)D * RL;                       // [D][RL]
-    double* sa = sg + (int64_t)D * RL;                       // [RL]
-    double* sw = sa + RL;                                     // [RL] (GF)
+    // LDS rows, chunk-major: 64-row chunks of kLF fields (x[D], g[D], A[, w]) x 64 doubles, so a
+    // row's fields lie 64 doubles apart -- one address per row, the fields at immediate offsets
+    // (ds_read2st64_b64 pairs them) instead of a runtime-stride address per coordinate
+    constexpr int kLF = 2 * D + 1 + (GF ? 1 : 0);
+    double* const srow0 = lds + (sizeof(Scratch) + 15) / 16 * 2;
+    auto lrow = [&](int e) -> double* { return srow0 + (e >> 6) * (kLF * 64) + (e & 63); };
+    constexpr int fX = 0, fG = D * 64, fA = 2 * D * 64, fW = (2 * D + 1) * 64;   // field offsets
     const int tid = threadIdx.x;
     const int64_t ld = a.ld;
     const int64_t r0 = a.row_begin + (int64_t)blockIdx.x * a.rows_per_block;
@@ -646,7 +656,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     // (stein_math.hpp fast_range_ok; padding rows are zeros)
     // wide d: x in registers, g in LDS (sgw[k][NT], where the LDS rows would start: RL = 0)
     double xr[RT > 0 ? RT : 1][D], gr[RT > 0 ? RT : 1][kWide ? 1 : D], ar[RT > 0 ? RT : 1];
-    double* sgw = sx;
+    double* sgw = srow0;
     double wr[(GF && RT > 0) ? RT : 1];
     int rok = scale_in_range(l, tr);
 #pragma unroll
@@ -670,11 +680,11 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
 #pragma unroll
             for (int k = 0; k < D; ++k) {
                 const double xv = ok ? a.x[k * ld + row] : 0.0, gv = ok ? a.g[k * ld + row] : 0.0;
-                sx[k * RL + e] = xv;
-                sg[k * RL + e] = gv;
+                lrow(e)[fX + k * 64] = xv;
+                lrow(e)[fG + k * 64] = gv;
                 rok &= fast_range_ok(xv) & fast_range_ok(gv);
             }
-            if constexpr (GF) sw[e] = ok ? a.w[row] : 0.0;
+            if constexpr (GF) lrow(e)[fW] = ok ? a.w[row] : 0.0;
         }
         for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
 #pragma unroll
@@ -712,11 +722,11 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             const int64_t row = lds_base + e;
             double gi[D], xi[D];
 #pragma unroll
-            for (int k = 0; k < D; ++k) { gi[k] = sg[k * RL + e]; xi[k] = sx[k * RL + e]; }
+            for (int k = 0; k < D; ++k) { gi[k] = lrow(e)[fG + k * 64]; xi[k] = lrow(e)[fX + k * 64]; }
             double kv = CMP ? diag_value_sel<D>(lok && row_in_range<D>(xi, gi), gi, tr) : diag_value_ct<D>(gi, tr);
-            if constexpr (GF) kv = (kv * sw[e]) * sw[e];
+            if constexpr (GF) kv = (kv * lrow(e)[fW]) * lrow(e)[fW];
             kv = row < r1 ? kv : INFINITY;
-            sa[e] = kv;
+            lrow(e)[fA] = kv;
             scan_take(kv, (uint32_t)row, bv, bi);
         }
         for (int64_t row = str_base + tid; row < r1; row += kPBlock) {
@@ -831,14 +841,15 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             auto lds_pair = [&](int e) -> double {
                 const int64_t row = lds_base + e;
                 double xi[D], gi[D];
+                double* const rp = lrow(e);
 #pragma unroll
-                for (int k = 0; k < D; ++k) { xi[k] = sx[k * RL + e]; gi[k] = sg[k * RL + e]; }
+                for (int k = 0; k < D; ++k) { xi[k] = rp[fX + k * 64]; gi[k] = rp[fG + k * 64]; }
                 double kv = pair_ar<D, AR>(xi, gi, xj, gj, l, l2, m3l2, tr, jok);
-                if constexpr (GF) kv = (kv * sw[e]) * wj;
+                if constexpr (GF) kv = (kv * rp[fW]) * wj;
                 double av;
-                if constexpr (FAST) av = add_twice<true>(sa[e], kv);
-                else av = row < r1 ? add_twice<false>(sa[e], kv) : INFINITY;
-                sa[e] = av;
+                if constexpr (FAST) av = add_twice<true>(rp[fA], kv);
+                else av = row < r1 ? add_twice<false>(rp[fA], kv) : INFINITY;
+                rp[fA] = av;
                 return av;
             };
             // streamed rows: two per iteration, the next two rows' loads in flight meanwhile
@@ -871,6 +882,26 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                 // with the largest index
                 const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(
                     a.A + str_base, 0, ns > 0 ? (int)(ns * 8) : 0, 0x00020000);
+                // streamed rows through descriptors based at str_base: ONE 32-bit lane offset per
+                // row, the column offsets k * ld * 8 as SGPR operands (no 64-bit address per
+                // coordinate; the host keeps (d - 1) * ld * 8 + rows * 8 below 2^31).  Rows past r1
+                // read row str_base (their results are dropped).
+                const auto xrs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.x + str_base), 0,
+                                                                   0x7FFFFFFF, 0x00020000);
+                const auto grs = __builtin_amdgcn_make_buffer_rsrc(const_cast<double*>(a.g + str_base), 0,
+                                                                   0x7FFFFFFF, 0x00020000);
+                const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
+                    const_cast<double*>(GF ? a.w + str_base : a.x), 0, 0x7FFFFFFF, 0x00020000);
+                auto fetch = [&](int64_t row, SRow& r) {
+                    const int off = row < r1 ? (int)((row - str_base) * 8) : 0;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        r.x[k] = buf_load_f64(xrs, off, (int)(k * ld * 8));
+                        r.g[k] = buf_load_f64(grs, off, (int)(k * ld * 8));
+                    }
+                    r.a = buf_load_f64(arsrc, off, 0);
+                    r.w = GF ? buf_load_f64(wrs, off, 0) : 1.0;
+                };
                 auto take_stream = [&](int64_t row, double av) {
                     const bool in = row < r1;
                     typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
@@ -982,7 +1013,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     }
     for (int e = tid; e < RL; e += kPBlock) {
         const int64_t row = lds_base + e;
-        if (row < r1) a.A[row] = sa[e];
+        if (row < r1) a.A[row] = lrow(e)[fA];
     }
 }
 
@@ -1146,6 +1177,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     if (persistent_ws_bytes(d, G, pitch, nrep) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n_shard + G - 1) / G;
     if (wide && R > 256) return hipErrorNotSupported;   // wide: one register row per thread only
+    // streamed rows are addressed with 32-bit buffer offsets (column k at k * ld * 8 bytes)
+    if ((int64_t)(d - 1) * ld * 8 + (R + 64) * 8 >= 0x7FFFFFFFll) return hipErrorNotSupported;
     // auto: 512-thread blocks (two waves per SIMD, dynamic chunks) once a block has more rows than
     // one wave per SIMD keeps in registers comfortably (measured crossover 1e3 .. 2e3 rows per CU,
     // scripts/sweep_nt_crossover.sh)
