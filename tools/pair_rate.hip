@@ -1,7 +1,8 @@
 // Measurement probe (not product code): fp64 throughput of the persistent kernel's register-row
-// inner loop (pair_value_ct<4, FAST> + running-sum fma + argmin scan) at 2 / 3 / 4 waves per SIMD,
-// with no exchange: every "step" reads the next winner row from a small table (block-uniform) and
-// sweeps the thread's RT register rows.  Reports ns per row-step per CU.
+// inner loop (pair_value_ct<4, FAST> or the compact pair_compact_ct<4> + running-sum fma + argmin
+// scan) at 1 / 2 / 3 / 4 waves per SIMD and IL rows per scheduling group (sched_barrier every IL
+// rows), with no exchange: every "step" reads the next winner row from a small table (block-uniform)
+// and sweeps the thread's RT register rows.  Reports ns per row-step per CU.
 // Build: hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -o tools/pair_rate tools/pair_rate.hip
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -10,7 +11,7 @@
 
 using namespace st;
 
-template <int NT, int RT>
+template <int NT, int RT, bool CMP, int IL>
 __global__ __launch_bounds__(NT, 1) void rows_kernel(const double* x, const double* g, const double* wins,
                                                      int steps, double l, double tr, double* out) {
     constexpr int D = 4;
@@ -23,7 +24,7 @@ __global__ __launch_bounds__(NT, 1) void rows_kernel(const double* x, const doub
         for (int k = 0; k < D; ++k) { xr[q][k] = x[row * D + k]; gr[q][k] = g[row * D + k]; }
         ar[q] = 1.0;
     }
-    const double l2 = l * l;
+    const double l2 = l * l, m3l2 = -3.0 * l2;
     double bv = 0;
     uint32_t bq = 0;
     for (int t = 0; t < steps; ++t) {
@@ -36,12 +37,12 @@ __global__ __launch_bounds__(NT, 1) void rows_kernel(const double* x, const doub
         }
 #pragma unroll
         for (int q = 0; q < RT; ++q) {
-            const double kv = pair_value_ct<D, true>(xr[q], gr[q], xj, gj, l, l2, tr);
+            const double kv = CMP ? pair_compact_ct<D>(xr[q], gr[q], xj, gj, l, m3l2, tr)
+                                  : pair_value_ct<D, true>(xr[q], gr[q], xj, gj, l, l2, tr);
             ar[q] = add_twice<true>(ar[q], kv);
             if (q == 0) { bv = ar[q]; bq = 0; }
             else { const bool tk = ar[q] < bv; bv = tk ? ar[q] : bv; bq = tk ? q : bq; }
-            if (NT < 768 && (q & 1) == 1) __builtin_amdgcn_sched_barrier(0);
-            if (NT >= 768) __builtin_amdgcn_sched_barrier(0);
+            if ((q % IL) == IL - 1) __builtin_amdgcn_sched_barrier(0);
         }
         if (bv == -1.0) out[tid] = bq;   // keep the scan live
     }
@@ -53,22 +54,23 @@ __global__ __launch_bounds__(NT, 1) void rows_kernel(const double* x, const doub
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("%s\n", hipGetErrorString(e_)); return 1; } } while (0)
 
-template <int NT, int RT>
+template <int NT, int RT, bool CMP, int IL>
 static int run(const double* x, const double* g, const double* w, double* out, int steps) {
     hipEvent_t a, b;
     hipEventCreate(&a);
     hipEventCreate(&b);
-    rows_kernel<NT, RT><<<256, NT>>>(x, g, w, 10, 0.37, 1.48, out);
+    rows_kernel<NT, RT, CMP, IL><<<256, NT>>>(x, g, w, 10, 0.37, 1.48, out);
     CK(hipDeviceSynchronize());
     hipEventRecord(a);
-    rows_kernel<NT, RT><<<256, NT>>>(x, g, w, steps, 0.37, 1.48, out);
+    rows_kernel<NT, RT, CMP, IL><<<256, NT>>>(x, g, w, steps, 0.37, 1.48, out);
     hipEventRecord(b);
     CK(hipEventSynchronize(b));
     float ms;
     hipEventElapsedTime(&ms, a, b);
     const double rows_per_cu = (double)NT * RT;
-    printf("NT=%4d RT=%2d rows/CU=%5.0f  %8.3f ms  %6.3f ns per row-step per CU  %.3f us per 7812-row step\n", NT,
-           RT, rows_per_cu, ms, ms * 1e6 / steps / rows_per_cu, ms * 1e3 / steps / rows_per_cu * 7812);
+    printf("%s NT=%4d RT=%2d IL=%d rows/CU=%5.0f  %8.3f ms  %6.3f ns per row-step per CU  %.3f us per 7812-row step\n",
+           CMP ? "compact" : "exact  ", NT, RT, IL, rows_per_cu, ms, ms * 1e6 / steps / rows_per_cu,
+           ms * 1e3 / steps / rows_per_cu * 7812);
     return 0;
 }
 
@@ -94,12 +96,18 @@ int main() {
     fill<<<8, 64>>>(w, 64 * 8, 3, 4.0);
     CK(hipDeviceSynchronize());
     const int steps = 2000;
-    run<256, 16>(x, g, w, out, steps);
-    run<512, 8>(x, g, w, out, steps);
-    run<512, 4>(x, g, w, out, steps);
-    run<768, 5>(x, g, w, out, steps);
-    run<768, 4>(x, g, w, out, steps);
-    run<1024, 4>(x, g, w, out, steps);
-    run<1024, 2>(x, g, w, out, steps);
+    run<512, 8, false, 2>(x, g, w, out, steps);
+    run<256, 16, true, 1>(x, g, w, out, steps);
+    run<256, 16, true, 2>(x, g, w, out, steps);
+    run<256, 16, true, 4>(x, g, w, out, steps);
+    run<256, 16, true, 8>(x, g, w, out, steps);
+    run<512, 8, true, 1>(x, g, w, out, steps);
+    run<512, 8, true, 2>(x, g, w, out, steps);
+    run<512, 8, true, 4>(x, g, w, out, steps);
+    run<512, 8, true, 8>(x, g, w, out, steps);
+    run<768, 5, true, 1>(x, g, w, out, steps);
+    run<768, 5, true, 5>(x, g, w, out, steps);
+    run<1024, 4, true, 1>(x, g, w, out, steps);
+    run<1024, 4, true, 2>(x, g, w, out, steps);
     return 0;
 }
