@@ -188,7 +188,8 @@ struct PersistArgs {
     int64_t m;            // n_points
     uint32_t* idx_out;
     uint64_t* gran;       // 2 banks x G records x 2 granules
-    unsigned* status;     // [0]: 0 ok, 1 timeout
+    unsigned* status;     // [0]: 0 ok, 1 timeout, 2 (compact-only kernel) a pair needs the exact arithmetic
+    const unsigned* gate; // general kernel after a compact-only one: run only if *gate == 2
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
     uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
@@ -606,7 +607,8 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             if (lane == 0) sc->rowfast = fast;
         }
         if (lane == 0) {
-            if (!ok_all) __hip_atomic_store(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // (max: a compact-only kernel's "needs the exact arithmetic" (2) is not overwritten)
+            if (!ok_all) __hip_atomic_fetch_max(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sc->abort = !ok_all;
             sc->i[0] = gi;
         }
@@ -620,9 +622,16 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
 // BPC = blocks per CU: 2 puts two 256-thread blocks on each CU (two waves per SIMD, RT <= 8
 // register rows each, every block its own record): the fp64 pipe issues from two waves.
 // CMP: the compact arithmetic for pairs in range (stein_math.hpp pair_compact_ct; st_tune key 11).
-template <int D, bool GF, int RT, int NT, int BPC, bool CMP>
+// GEN = false (with CMP): the compact-only kernel -- no exact / mixed sweep compiled in, which frees
+// the registers those paths need for more register rows.  A step that would need them (a block row
+// or the winner out of range, a NaN running sum) sets status 2 and every block leaves; the general
+// kernel, enqueued right behind it with gate = that status word, then runs the whole thin (and
+// returns at once when the compact-only run completed).  One device only.
+template <int D, bool GF, int RT, int NT, int BPC, bool CMP, bool GEN = true>
 __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     static_assert(!CMP || D <= kMaxCtDim, "compact arithmetic: d <= 8 only");
+    static_assert(GEN || CMP, "the compact-only kernel is a compact kernel");
+    if (a.gate && *a.gate != 2u) return;   // general kernel behind a compact-only run that finished
     constexpr int kPBlock = NT;
     constexpr int kMaxG = 256 * BPC;     // records swept per step
     constexpr bool kTwoWaves = NT >= 512 || BPC > 1;   // two waves per SIMD
@@ -987,8 +996,14 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
         };
         // the flag is block-uniform (same LDS row, same block flag): make that explicit so the
         // branch is scalar and the two variants stay separate code paths
-        if (__builtin_amdgcn_readfirstlane(wfast)) sweep_rows(std::integral_constant<int, CMP ? 2 : 1>{});
-        else sweep_rows(std::integral_constant<int, CMP ? 3 : 0>{});
+        if (__builtin_amdgcn_readfirstlane(wfast)) {
+            sweep_rows(std::integral_constant<int, CMP ? 2 : 1>{});
+        } else if constexpr (!GEN) {   // compact-only: hand the thin to the general kernel
+            if (tid == 0) __hip_atomic_fetch_max(a.status, 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            break;
+        } else {
+            sweep_rows(std::integral_constant<int, CMP ? 3 : 0>{});
+        }
         ST_STAMP(a, t, 3);
         publish<NT>(a, sc, bv, bi, t, r1);
         ST_STAMP(a, t, 4);
@@ -1039,6 +1054,13 @@ static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (on
 static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
 static int g_persist_pitch = -1; // st_tune key 9: record pitch in bytes (16 .. 4096, power of 2), -1 auto
 static int g_persist_nrep = -1;  // st_tune key 10: record replicas (1 .. 32, power of 2), -1 auto
+static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register rows (8 .. 10), 0 off, -1 auto
+// automatic register rows of the compact-only kernel: 9 (28 B of scratch at d = 4) unless more than
+// kCmpStreamRows rows per block would still be streamed, then 10 (108 B of scratch; the streamed
+// rows then no longer stay in the XCD's L2).  Same-box, d = 4, m = 1000 (profiles/r03_compact_only_rt.log):
+// n = 2e6: 7.81 (general kernel) / 7.76 (8) / 7.05 (9) / 7.29 (10) us per step; n = 3e6: 19.8 /
+// 19.7 / 18.5 / 17.8.
+constexpr int64_t kCmpStreamRows = 2048;
 static uint64_t* g_stamps = nullptr;
 #ifdef ST_PERSIST_STAMPS
 extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
@@ -1074,14 +1096,23 @@ int persistent_tune(int key, int value) {
         g_persist_nrep = value;
         return 0;
     }
+    if (key == 12) {
+        if (value != -1 && value != 0 && (value < 8 || value > 10)) return -1;
+        g_persist_cmp = value;
+        return 0;
+    }
     return -1;
 }
 
-template <int D, bool GF, int RT, int NT, int BPC = 1>
+template <int D, bool GF, int RT, int NT, int BPC = 1, bool GEN = true>
 static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s, bool dry) {
-    // the compact instantiation for d <= 8 when st_tune key 11 selects it (the default)
-    auto fn = (D <= kMaxCtDim && arith_compact()) ? greedy_persistent<D, GF, RT, NT, BPC, D <= kMaxCtDim>
-                                                  : greedy_persistent<D, GF, RT, NT, BPC, false>;
+    // the compact instantiation for d <= 8 when st_tune key 11 selects it (the default); GEN = false:
+    // the compact-only kernel (launch_greedy_persistent enqueues the general one behind it)
+    void (*fn)(PersistArgs);
+    if constexpr (!GEN) fn = greedy_persistent<D, GF, RT, NT, BPC, true, false>;
+    else if constexpr (D <= kMaxCtDim)
+        fn = arith_compact() ? greedy_persistent<D, GF, RT, NT, BPC, true> : greedy_persistent<D, GF, RT, NT, BPC, false>;
+    else fn = greedy_persistent<D, GF, RT, NT, BPC, false>;
     hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
@@ -1107,6 +1138,14 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     return hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs, lds, s);
 }
 
+// compact-only kernels: 512-thread blocks, 8 / 9 / 10 register rows per thread
+template <int D, bool GF>
+static hipError_t launch_p_cmp(const PersistArgs& a, int rt, int G, size_t lds, hipStream_t s, bool dry) {
+    if (rt >= 10) return launch_p<D, GF, 10, 512, 1, false>(a, G, lds, s, dry);
+    if (rt == 9) return launch_p<D, GF, 9, 512, 1, false>(a, G, lds, s, dry);
+    return launch_p<D, GF, 8, 512, 1, false>(a, G, lds, s, dry);
+}
+
 template <int D, bool GF>
 static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int G, size_t lds, hipStream_t s,
                                bool dry) {
@@ -1124,6 +1163,12 @@ static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int
         case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s, dry);
         default: return launch_p<D, GF, 16, 256>(a, G, lds, s, dry);
     }
+}
+
+static hipError_t launch_cmp(const PersistArgs& a, int d, bool gf, int rt, int G, size_t lds, hipStream_t s,
+                             bool dry) {
+    if (d == 2) return gf ? launch_p_cmp<2, true>(a, rt, G, lds, s, dry) : launch_p_cmp<2, false>(a, rt, G, lds, s, dry);
+    return gf ? launch_p_cmp<4, true>(a, rt, G, lds, s, dry) : launch_p_cmp<4, false>(a, rt, G, lds, s, dry);
 }
 
 static hipError_t launch_kind(const PersistArgs& a, int d, bool wide, bool gf, int rt, int nt, int bpc, int G,
@@ -1229,9 +1274,36 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.seq_base = rs->seq_base;
     a.inbox = rs->inbox;
     for (int r = 0; r < kMaxRanks; ++r) a.peer[r] = r < rs->nranks ? rs->peer[r] : nullptr;
+    // one device, 512-thread blocks with at least 8 register rows' worth of rows per block: the
+    // compact-only kernel (more register rows per thread, fewer streamed rows) runs the thin first and
+    // the general kernel, enqueued behind it, runs only if a step needed the exact arithmetic (its
+    // gate is the compact-only kernel's status word, its own status the next word)
+    PersistArgs ac = a;
+    bool use_cmp = false;
+    int rt_c = 0;
+    size_t lds_c = 0;
+    if (rs->nranks == 1 && arith_compact() && nt == 512 && bpc == 1 && !wide && g_persist_cmp != 0 &&
+        R >= 8 * 512) {
+        const int64_t rl_cap = (int64_t)((budget - head) / row_bytes) / 64 * 64;
+        rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R - 9 * 512 - rl_cap > kCmpStreamRows ? 10 : 9);
+        while (rt_c > 8 && (int64_t)rt_c * 512 > R) --rt_c;   // no empty register rows
+        int64_t RLc = (int64_t)((budget - head) / row_bytes);
+        const int64_t need_c = R - (int64_t)rt_c * 512;
+        if (RLc > need_c) RLc = need_c > 0 ? need_c : 0;
+        RLc = RLc / 64 * 64;
+        ac.RL = (int)RLc;
+        lds_c = head + (size_t)RLc * row_bytes;
+        use_cmp = launch_cmp(ac, d, gf, rt_c, G, lds_c, s, true) == hipSuccess;   // residency check only
+    }
     // zero status and every granule tag (a stale tag from a previous run must never match)
     hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G, pitch, nrep), s);
     if (e != hipSuccess) return e;
+    if (use_cmp) {
+        e = launch_cmp(ac, d, gf, rt_c, G, lds_c, s, false);
+        if (e != hipSuccess) return e;
+        a.gate = ac.status;
+        a.status = ac.status + 1;
+    }
     e = launch_kind(a, d, wide, gf, rt, nt, bpc, G, lds, s, false);
     if (e == hipSuccess) *used = 1;
     return e;

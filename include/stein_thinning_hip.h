@@ -69,7 +69,10 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * (1 = compact, the default: the kernel value regrouped around one reciprocal square root, a few
  * ulps from NumPy's evaluation, for every pair whose two rows and l, tr lie in [2^-60, 2^60];
  * 0 = exact: NumPy's evaluation order rounding for rounding; other pairs are always exact -- see
- * oracle/stein_ref.c and DESIGN.md §3; all ranks of a sharded run must use the same value).
+ * oracle/stein_ref.c and DESIGN.md §3; all ranks of a sharded run must use the same value), key 12 =
+ * register rows per thread of the one-device compact-only persistent kernel (8 .. 10; 0 = do not use
+ * it; -1 = automatic: 9, or 10 when more than 2048 rows per block would still be streamed; fewer
+ * when a block has fewer rows).
  */
 int st_tune(int32_t key, int32_t value);
 

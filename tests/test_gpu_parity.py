@@ -301,6 +301,46 @@ def test_persistent_exact_path_outside_fast_range(d, gf, steps, mode):
         assert np.intersect1d(idx, rows[:6]).size > 0
 
 
+@pytest.mark.parametrize('case', ['in_range', 'tiny_rows_one_block', 'tiny_scores_selected', 'gf_inf_weights'])
+def test_compact_only_kernel_and_handoff(case):
+    """n = 1.1e6 rows (more than 8 register rows' worth per 512-thread block): the one-device
+    compact-only persistent kernel (st_tune key 12) runs the thin; when a step needs the exact
+    arithmetic -- rows out of [2^-60, 2^60] in one block, an out-of-range row selected, NaN sums
+    from infinite gradient-free weights -- it hands the whole thin to the general kernel enqueued
+    behind it.  Indices and running sums bit-identical to the C model and to the general kernel
+    alone (key 12 = 0), whichever kernel finished the run."""
+    from stein_thinning import _native
+    n, m, d = 1_100_003, 30, 4
+    x, g = _rw_chain(n, d, seed=31)
+    s, gs = o._validate_and_standardize(x, g, True)
+    s, gs = s.copy(), gs.copy()
+    w = None
+    if case == 'tiny_rows_one_block':
+        s[500_000:500_010, 1] = 1e-30          # ten rows of one block, never near the minimum
+    elif case == 'tiny_scores_selected':
+        gs[[7, 800_001], :] = 3e-22            # smallest diagonals: selected at once
+    elif case == 'gf_inf_weights':
+        lw = -0.2 * np.sum(x * x, axis=1)
+        lw[[123, 900_000]] = 900.0             # exp overflows: inf weights -> NaN running sums
+        with np.errstate(over='ignore'):
+            w = np.exp(lw - lw.min())
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    prob = DeviceProblem(s, gs, w, l, tr)
+    idx, A = prob.greedy(m, return_sums=True)
+    cidx, cA = oracle_c.greedy_mt(s, gs, w, l, tr, m)
+    np.testing.assert_array_equal(idx, cidx)
+    assert np.array_equal(A, cA, equal_nan=True), np.flatnonzero(~((A == cA) | (np.isnan(A) & np.isnan(cA))))[:10]
+    L = _native.lib()
+    assert L.st_tune(12, 0) == 0
+    try:
+        gidx, gA = prob.greedy(m, return_sums=True)
+    finally:
+        L.st_tune(12, -1)
+    np.testing.assert_array_equal(gidx, idx)
+    assert np.array_equal(gA, A, equal_nan=True)
+
+
 @pytest.mark.parametrize('d', [2, 4, 9, 50])
 def test_pair_values_bit_exact_vs_c_model(d):
     x, g = _rw_chain(700, d, seed=100 + d)

@@ -165,6 +165,13 @@ int main(int argc, char** argv) {
     st_tune(0, 256); st_tune(1, -1); st_tune(2, -1);
     if (argc > 2 && argv[2][0] == 'q') {   // quick: the default persistent configuration, m = 1000
         const int Mq = 1000;
+        // optional st_tune overrides: PROBE_NT (key 4), PROBE_RT (key 3), PROBE_GRID (key 5), PROBE_NREP (key 10),
+        // PROBE_CMP (key 12)
+        if (getenv("PROBE_NT")) st_tune(4, atoi(getenv("PROBE_NT")));
+        if (getenv("PROBE_RT")) st_tune(3, atoi(getenv("PROBE_RT")));
+        if (getenv("PROBE_GRID")) st_tune(5, atoi(getenv("PROBE_GRID")));
+        if (getenv("PROBE_NREP")) st_tune(10, atoi(getenv("PROBE_NREP")));
+        if (getenv("PROBE_CMP")) st_tune(12, atoi(getenv("PROBE_CMP")));
         std::vector<float> v;
         std::vector<uint32_t> h(Mq);
         for (int rep = 0; rep < 5; ++rep) {
