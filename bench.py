@@ -118,6 +118,23 @@ def _persistent_nt(n_shard: int, d: int) -> int:
     return 512 if d in (2, 4) and rows_per_block > 1280 else 256
 
 
+def _persistent_label(n_shard: int, d: int, gf: bool, arithmetic: str, world: int) -> str:
+    """The persistent kernel launch_greedy_persistent enqueues by default (persistent.hip): one device,
+    512-thread blocks and at least 4 096 rows per block under the compact arithmetic -> the
+    compact-only kernel (9 register rows per thread, 10 when more than 2 048 rows per block would
+    still be streamed) with the general kernel gated behind it."""
+    nt = _persistent_nt(n_shard, d)
+    rows = -(-n_shard // 256)
+    g = str(gf).lower()
+    if world == 1 and nt == 512 and arithmetic == 'compact' and rows >= 8 * 512:
+        row_bytes = (2 * d + 1 + (1 if gf else 0)) * 8
+        rl_cap = (163840 - 1024 - 256) // row_bytes // 64 * 64
+        rt = 10 if rows - 9 * 512 - rl_cap > 2048 else 9
+        return (f'greedy_persistent<{d},{g},{rt},512,1,compact,compact-only> (+ the general kernel gated behind '
+                f'it: returns at once)')
+    return f'greedy_persistent<{d},{g},RT,{nt}>'
+
+
 def make_integrand(cfg):
     import warnings
     from stein_thinning import thinning as st
@@ -413,11 +430,11 @@ def main():
             roofline = {
                 'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
                 'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': traffic,
-                'kernel': f'greedy_persistent<{d},{str(gf).lower()},RT,{_persistent_nt(n // world, d)}>'
+                'kernel': _persistent_label(n // world, d, gf, arithmetic, world)
                           + (f' x{world} ranks' if sharded else ''),
                 'kernel_median_us': round(med * 1e6, 1), 'kernel_avg_us': round(avg * 1e6, 1),
                 'timing': f'median of HIP events on the launch stream around each of the {args.steps} timed '
-                          'thins (one persistent launch each)' + (', max over ranks' if sharded else ''),
+                          'thins (the persistent launch(es) of one thin)' + (', max over ranks' if sharded else ''),
                 'flop_per_pair': flop_per_pair,
                 'flop_per_pair_source': 'SURVEY.md 8(d): 12 d + 40 (+2 gradient-free), algorithmic',
                 'issue': {'fp64_instr_per_pair': instr_per_pair, 'isa_flop_per_pair': issue_flop_per_pair,
