@@ -674,6 +674,8 @@ def main_ksd(args):
     cfg = CONFIGS[args.config if args.config != 'c4' or args.ksd_full else 'c2']
     integrand, _, _ = make_integrand(cfg)
     n, d = cfg['n'], integrand.sample.shape[1]
+    import stein_thinning
+    stein_thinning.set_arithmetic(args.arith)
     be = sd.HipKsdBackend(integrand, n)
     a0, a1 = sd.triangle_row_bounds(n, rank, world)
     ks = torch.empty(n, dtype=torch.float64, device=dev)
@@ -720,7 +722,13 @@ def main_ksd(args):
     rank_pairs = sum(n - 1 - a for a in range(a0, a1)) if n < 10 ** 4 else \
         (a1 - a0) * (n - 1) - (a1 * (a1 - 1) - a0 * (a0 - 1)) // 2
     flop_per_pair = algorithmic_flop_per_pair(d, gf) + 1     # + the column accumulate
-    isa_flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0) + 1
+    # the column-sum kernel's ISA flop per pair: compact arithmetic (default, d <= 8) 67 - 2 (the
+    # running-sum fma is the plain accumulate here) + 8 per further coordinate; exact 134 + 13 per
+    # coordinate; + the weights' 2 mul, + the accumulate
+    if args.arith == 'compact' and d <= 8:
+        isa_flop_per_pair = 65 + 8 * (d - 4) + (2 if gf else 0) + 1
+    else:
+        isa_flop_per_pair = 134 + 13 * (d - 4) + (2 if gf else 0) + 1
     if rank == 0:
         tflops = rank_pairs * flop_per_pair / colsum_s / 1e12
         line = {
@@ -731,6 +739,7 @@ def main_ksd(args):
             'data': 'synthetic (seeded RW-MH LV-surrogate chains; see bench.py docstring)',
             'config': {'workload': f"full-sample KSD of config {cfg['desc']}", 'n': n, 'd': d,
                        'kernel': 'gradient-free' if gf else 'langevin',
+                       'arithmetic': args.arith if d <= 8 else 'exact',
                        'parallelism': f'triangle rows x{world}, RCCL all-reduce of the n-vector' if world > 1
                        else 'single-gpu'},
             'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS,

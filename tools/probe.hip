@@ -242,6 +242,7 @@ int main(int argc, char** argv) {
         if (getenv("PROBE_NT")) st_tune(4, atoi(getenv("PROBE_NT")));
         if (getenv("PROBE_RT")) st_tune(3, atoi(getenv("PROBE_RT")));
         if (getenv("PROBE_NREP")) st_tune(10, atoi(getenv("PROBE_NREP")));
+        if (getenv("PROBE_CMP")) st_tune(12, atoi(getenv("PROBE_CMP")));
         uint64_t* dst;
         CK(hipMalloc(&dst, sizeof(uint64_t) * GMAX * SP * PH));
         CK(hipMemset(dst, 0, sizeof(uint64_t) * GMAX * SP * PH));
