@@ -348,9 +348,12 @@ __global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
                 double dist;
                 if constexpr (FAST) {
                     // the compiler's sqrt sequence without its scaling (ss >= 2^-767) and class
-                    // fix-up (only 0 and inf): the same bits as __builtin_sqrt in this range
+                    // fix-up (only 0 and inf): the same bits as __builtin_sqrt in this range.  A
+                    // zero distance takes the sqrt of 2^-224 and is selected away afterwards, so the
+                    // loop has no branch (a conditional sqrt was compiled as an exec-mask branch)
                     double h;
-                    dist = ss == 0.0 ? 0.0 : fast_sqrt(ss, h);
+                    const double r = fast_sqrt(__builtin_fmax(ss, 0x1p-224), h);
+                    dist = ss == 0.0 ? 0.0 : r;
                 } else {
                     dist = __builtin_sqrt(ss);
                 }
