@@ -125,3 +125,13 @@ def test_tune_keys_validate_without_gpu(libpath):
             assert lib.st_tune(key, v) != 0, (key, v)
         assert lib.st_tune(key, -1) == 0
     assert lib.st_tune(99, 1) != 0
+
+
+def test_set_arithmetic_is_host_only_and_validates(libpath):
+    """stein_thinning.set_arithmetic (st_tune key 11) records a host-side knob: both modes are
+    accepted without a GPU, anything else is rejected before reaching the library."""
+    import stein_thinning
+    with pytest.raises(ValueError):
+        stein_thinning.set_arithmetic('fast')
+    stein_thinning.set_arithmetic('exact')
+    stein_thinning.set_arithmetic('compact')
