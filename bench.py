@@ -471,6 +471,27 @@ def main():
                             'timing': 'HIP events around back-to-back single-step launches'}
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(cfg, integrand, args.cpu_steps, result_idx, arithmetic)
+        exact = None
+        if world == 1 and not sharded and d <= 8 and arithmetic == 'compact':
+            # the same thin with the exact arithmetic (NumPy's evaluation order; not `value`): its
+            # time and whether it selects the same indices as the timed compact run
+            import stein_thinning
+            stein_thinning.set_arithmetic('exact')
+            try:
+                run_once()
+                ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+                for e0, e1 in ev:
+                    e0.record(stream)
+                    run_once()
+                    e1.record(stream)
+                torch.cuda.synchronize()
+                exact_idx = idx.cpu().numpy().view(np.uint32)
+                exact = {'ms_per_thin': round(float(np.median([a.elapsed_time(b) for a, b in ev])), 4),
+                         'same_indices_as_timed_run': bool(np.array_equal(exact_idx, result_idx))}
+            finally:
+                stein_thinning.set_arithmetic('compact')
+                run_once()   # leave the buffers as the timed (compact) run left them
+                torch.cuda.synchronize()
         e2e = None
         if world == 1 and not cfg['gf'] and not cfg.get('d50'):
             # the drop-in call on host arrays (not `value`): standardisation + 'med' + H2D upload +
@@ -522,6 +543,7 @@ def main():
             'roofline': roofline,
             'cpu_baseline': cpu,
             'end_to_end': e2e if rank == 0 and not sharded else None,
+            'exact_arithmetic': exact if rank == 0 and not sharded else None,
         }
         print(json.dumps(line), flush=True)
     if sharded:
