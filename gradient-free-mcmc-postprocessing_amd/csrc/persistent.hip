@@ -331,6 +331,21 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
     }
 }
 
+// Polls are issued on a chip-wide grid of ST_POLL_SYNC ticks of s_memrealtime (100 MHz: 450 ns).
+// Every block then sees the last record of a step at about the same moment and starts the next
+// step together, instead of each at its own poll phase (the spread of next-step starts was about
+// one poll period, ~1.1 us, and the latest starter bounds the next exchange).  Same-box, three
+// rounds (profiles/r03_poll_sync.log): n = 2e6 7.06 -> 6.83 us per step, n = 1e6 5.06 -> 4.97,
+// n = 2.5e5 (the 8-GPU shard size) 3.30 -> 3.17; grids of 300 / 380 / 520 / 600 / 800 / 1100 /
+// 1300 ns, and leaving the first poll of a step unaligned, were measured beside it (coarser grids
+// quantise the step: 1.3 us made n = 2.5e5 3.9 us per step).
+#ifndef ST_POLL_SYNC
+#define ST_POLL_SYNC 45
+#endif
+#ifndef ST_POLL_SYNC_FIRST
+#define ST_POLL_SYNC_FIRST 1
+#endif
+
 // wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
 // (np.argmin order).  Lane L owns records L, L+64, L+128, L+192 and re-polls only those it has not
 // seen yet.  Whenever its best-so-far changes it loads that candidate's row (x, g[, w]) from the
@@ -451,6 +466,13 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
 #endif
         for (;;) {
             u32x4 qs[MAXG / 64];
+#if ST_POLL_SYNC > 0
+            if (ST_POLL_SYNC_FIRST || it > 0) {   // polls on a chip-wide grid of ST_POLL_SYNC ticks
+                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                const uint64_t slot = (now + ST_POLL_SYNC - 1) / ST_POLL_SYNC * ST_POLL_SYNC;
+                while (__builtin_amdgcn_s_memrealtime() < slot) __builtin_amdgcn_s_sleep(1);
+            }
+#endif
             issue(qs);
             if (it > 0) {   // no memory access: runs while the loads above are in flight
                 double rv;

@@ -6,7 +6,7 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-for r in 1 2; do
+for r in ${PV_ROUNDS:-1 2}; do
   for n in ${PV_NS:-2000000 250000}; do
     for v in "$@"; do
       echo "## $v n=$n round $r"
