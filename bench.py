@@ -306,6 +306,7 @@ def main():
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
     ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
     ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
+    ap.add_argument('--energy-variant', type=int, default=0, help='energy kernel (st_tune key 13; 0 = auto)')
     ap.add_argument('--arith', default='compact', choices=['compact', 'exact'],
                     help='arithmetic of the d <= 8 greedy kernels (stein_thinning.set_arithmetic)')
     ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks'],
@@ -580,6 +581,8 @@ def main_energy(args):
     # `cached` below: the reference's loop over methods x chains, where that triangle is computed
     # once per validation sample (stein_thinning.energy.PointSet) and a curve is the cross block and
     # the selection's triangle
+    from stein_thinning import _native as nat
+    nat.check(nat.lib().st_tune(13, args.energy_variant), 'st_tune')
     curve = se.EnergyCurve(validation, x[idx], cache_reference=False)
     pairs = curve.pair_count()
     curve_c = se.EnergyCurve(validation, x[idx])
@@ -637,7 +640,7 @@ def main_energy(args):
             'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
                          'frac': round(tflops / FP64_VALU_PEAK_TFS, 4),
                          'traffic': pmc_traffic('energy') if world == 1 else None,
-                         'kernel': f'dist_colsum_kernel<{d}> (+ reduce / cumsum)', 'step_median_us': round(step_s * 1e6, 1),
+                         'kernel': f'dist_colsum_kernel<{d},U,MINB> variant {args.energy_variant} (+ reduce / cumsum)', 'step_median_us': round(step_s * 1e6, 1),
                          'flop_per_pair': flop_pair,
                          'note': 'per pair: d differences, squares and sums, one correctly rounded sqrt (the '
                                  'range-guarded ~10-instruction sequence, one quarter-rate v_rsq_f64) and the '

@@ -81,6 +81,7 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks) {
 int st_tune(int32_t key, int32_t value) {
     int rc;
     if (key == 7) rc = st::proxy_tune(value);
+    else if (key == 13) rc = st::dist_tune(value);
     else rc = ((key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12) ? st::persistent_tune(key, value)
                                                                                           : st::tune(key, value);
     if (rc != 0) return fail(ST_ERR_INVALID, "bad tuning key/value %d=%d", key, value);

@@ -299,8 +299,11 @@ __device__ __forceinline__ void dist_range(const DistArgs& p, int64_t c0, int64_
     if (p.tri && c0 + cols < hi) hi = c0 + cols;
 }
 
-template <int D>
-__global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
+// U: independent partial sums per thread in full below-diagonal tiles (U pairs in flight, U sqrt
+// chains interleaved; the partials are added at the end -- a different but deterministic order, the
+// energy curve is checked to a tolerance, not bitwise); MINB: blocks per CU the compiler budgets for
+template <int D, int U, int MINB>
+__global__ __launch_bounds__(kColBlock, MINB) void dist_colsum_kernel(DistArgs p) {
     constexpr int R = kColBlock;
     __shared__ double sb[D][R];
     const int tid = threadIdx.x;
@@ -336,8 +339,39 @@ __global__ __launch_bounds__(kColBlock, 4) void dist_colsum_kernel(DistArgs p) {
         const bool fast = __syncthreads_and(tok) != 0;
         const int cnt = (int)((b_stop - bc) < R ? (b_stop - bc) : R);
         const bool below = !p.tri || bc + cnt <= c0;
+        auto pair_dist = [&](int e, auto fast_tag) -> double {
+            constexpr bool FAST = decltype(fast_tag)::value;
+            double ss = 0.0;
+#pragma unroll
+            for (int k = 0; k < D; ++k) {
+                const double dk = ai[k] - sb[k][e];
+                ss += dk * dk;
+            }
+            if constexpr (FAST) {
+                double h;
+                const double r = fast_sqrt(__builtin_fmax(ss, 0x1p-224), h);
+                return ss == 0.0 ? 0.0 : r;
+            } else {
+                return __builtin_sqrt(ss);
+            }
+        };
         auto tile = [&](auto fast_tag, auto below_tag) {
             constexpr bool FAST = decltype(fast_tag)::value, BELOW = decltype(below_tag)::value;
+            if constexpr (BELOW && U > 1) {
+                double part[U];
+#pragma unroll
+                for (int u = 0; u < U; ++u) part[u] = 0.0;
+                int e = 0;
+                for (; e + U <= cnt; e += U) {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) part[u] += pair_dist(e + u, fast_tag);
+                }
+                for (; e < cnt; ++e) part[0] += pair_dist(e, fast_tag);
+#pragma unroll
+                for (int u = 1; u < U; ++u) part[0] += part[u];
+                acc = acc + part[0];
+                return;
+            }
             for (int e = 0; e < cnt; ++e) {
                 double ss = 0.0;
 #pragma unroll
@@ -414,6 +448,26 @@ __global__ void dist_reduce_kernel(const double* part, int64_t na, int K, double
     out[i] = acc;
 }
 
+// st_tune key 13: energy kernel variant (0 / -1 auto; 1: one partial sum, 4 blocks per CU -- round 2;
+// 2: U = 2, 4 blocks; 3: U = 1, 8 blocks; 4: U = 2, 8 blocks; 5: U = 4, 4 blocks)
+static int g_dist_variant = 0;
+int dist_tune(int value) {
+    if (value < -1 || value > 5) return -1;
+    g_dist_variant = value < 0 ? 0 : value;
+    return 0;
+}
+
+template <int D>
+static void launch_dist_ct(const DistArgs& p, dim3 grid, hipStream_t s) {
+    switch (g_dist_variant) {
+        case 2: dist_colsum_kernel<D, 2, 4><<<grid, kColBlock, 0, s>>>(p); break;
+        case 3: dist_colsum_kernel<D, 1, 8><<<grid, kColBlock, 0, s>>>(p); break;
+        case 4: dist_colsum_kernel<D, 2, 8><<<grid, kColBlock, 0, s>>>(p); break;
+        case 5: dist_colsum_kernel<D, 4, 4><<<grid, kColBlock, 0, s>>>(p); break;
+        default: dist_colsum_kernel<D, 1, 4><<<grid, kColBlock, 0, s>>>(p); break;
+    }
+}
+
 // B chunks per launch: enough blocks to fill the chip (>= 2048 over both grid dimensions) without
 // chunks shorter than four staging tiles (1024 points)
 int64_t distance_chunks(int64_t na, int64_t b_begin, int64_t b_end) {
@@ -438,14 +492,14 @@ hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, cons
     DistArgs p{a, lda, na, b, ldb, b0, b1, tri, K > 1 ? ws : out, chunk};
     const dim3 grid((unsigned)((na + kColBlock - 1) / kColBlock), (unsigned)K);
     switch (d) {
-        case 1: dist_colsum_kernel<1><<<grid, kColBlock, 0, s>>>(p); break;
-        case 2: dist_colsum_kernel<2><<<grid, kColBlock, 0, s>>>(p); break;
-        case 3: dist_colsum_kernel<3><<<grid, kColBlock, 0, s>>>(p); break;
-        case 4: dist_colsum_kernel<4><<<grid, kColBlock, 0, s>>>(p); break;
-        case 5: dist_colsum_kernel<5><<<grid, kColBlock, 0, s>>>(p); break;
-        case 6: dist_colsum_kernel<6><<<grid, kColBlock, 0, s>>>(p); break;
-        case 7: dist_colsum_kernel<7><<<grid, kColBlock, 0, s>>>(p); break;
-        case 8: dist_colsum_kernel<8><<<grid, kColBlock, 0, s>>>(p); break;
+        case 1: launch_dist_ct<1>(p, grid, s); break;
+        case 2: launch_dist_ct<2>(p, grid, s); break;
+        case 3: launch_dist_ct<3>(p, grid, s); break;
+        case 4: launch_dist_ct<4>(p, grid, s); break;
+        case 5: launch_dist_ct<5>(p, grid, s); break;
+        case 6: launch_dist_ct<6>(p, grid, s); break;
+        case 7: launch_dist_ct<7>(p, grid, s); break;
+        case 8: launch_dist_ct<8>(p, grid, s); break;
         default: dist_colsum_rt_kernel<<<grid, kColBlock, 0, s>>>(p, d); break;
     }
     if (K > 1) dist_reduce_kernel<<<(unsigned)((na + 255) / 256), 256, 0, s>>>(ws, na, (int)K, out);

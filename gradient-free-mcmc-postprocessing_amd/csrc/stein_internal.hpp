@@ -96,6 +96,7 @@ hipError_t launch_kde(const double* p, int64_t ldp, int64_t n, const double* log
                       double* log_q, double* grad, double* ws, hipStream_t s);
 hipError_t launch_proxy(const ProxyArgs& a, hipStream_t s);
 int proxy_tune(int value);   // st_tune key 7
+int dist_tune(int value);    // st_tune key 13 (energy kernel variant)
 
 struct LvArgs {
     const double* theta;      // (n, 4) row-major ODE parameters
