@@ -292,6 +292,24 @@ struct DistArgs {
     int64_t chunk;     // B points per blockIdx.y chunk (multiple of the staging tile)
 };
 
+// sqrt(ss) for ss = 0 or ss in [2^-224, 2^124] (the block-uniform fast range): the compiler's sqrt
+// sequence without its scaling (ss >= 2^-767) and class fix-up (only 0 and inf) -- the same bits as
+// __builtin_sqrt there -- with no branch (a conditional sqrt was compiled as an exec-mask branch).
+// ss = 0: rsq(0) = inf makes the sequence a quiet NaN, and fmin (IEEE minNum: the non-NaN operand)
+// returns ss * 2^200 = 0; ss > 0: ss * 2^200 = sqrt(ss)^2 * 2^200 >= sqrt(ss) since sqrt(ss) >=
+// 2^-112 > 2^-200 (and ss * 2^200 <= 2^324 is finite), so fmin returns the sqrt.  Two instructions instead of SEL's four
+// (fmax, compare, two 32-bit selects)
+template <bool SEL>
+__device__ __forceinline__ double fast_dist(double ss) {
+    double h;
+    if constexpr (SEL) {
+        const double r = fast_sqrt(__builtin_fmax(ss, 0x1p-224), h);
+        return ss == 0.0 ? 0.0 : r;
+    } else {
+        return __builtin_fmin(fast_sqrt(ss, h), ss * 0x1p200);
+    }
+}
+
 // B range of this block: chunk blockIdx.y of [b0, b1), cut at the block's last column for the triangle
 __device__ __forceinline__ void dist_range(const DistArgs& p, int64_t c0, int64_t cols, int64_t& lo, int64_t& hi) {
     lo = p.b0 + (int64_t)blockIdx.y * p.chunk;
@@ -302,7 +320,8 @@ __device__ __forceinline__ void dist_range(const DistArgs& p, int64_t c0, int64_
 // U: independent partial sums per thread in full below-diagonal tiles (U pairs in flight, U sqrt
 // chains interleaved; the partials are added at the end -- a different but deterministic order, the
 // energy curve is checked to a tolerance, not bitwise); MINB: blocks per CU the compiler budgets for
-template <int D, int U, int MINB>
+// SEL: the round-2 zero-distance form (fmax, compare, select) instead of the fmin form below
+template <int D, int U, int MINB, bool SEL = false>
 __global__ __launch_bounds__(kColBlock, MINB) void dist_colsum_kernel(DistArgs p) {
     constexpr int R = kColBlock;
     __shared__ double sb[D][R];
@@ -347,11 +366,8 @@ __global__ __launch_bounds__(kColBlock, MINB) void dist_colsum_kernel(DistArgs p
                 const double dk = ai[k] - sb[k][e];
                 ss += dk * dk;
             }
-            if constexpr (FAST) {
-                double h;
-                const double r = fast_sqrt(__builtin_fmax(ss, 0x1p-224), h);
-                return ss == 0.0 ? 0.0 : r;
-            } else {
+            if constexpr (FAST) return fast_dist<SEL>(ss);
+            else {
                 return __builtin_sqrt(ss);
             }
         };
@@ -381,13 +397,7 @@ __global__ __launch_bounds__(kColBlock, MINB) void dist_colsum_kernel(DistArgs p
                 }
                 double dist;
                 if constexpr (FAST) {
-                    // the compiler's sqrt sequence without its scaling (ss >= 2^-767) and class
-                    // fix-up (only 0 and inf): the same bits as __builtin_sqrt in this range.  A
-                    // zero distance takes the sqrt of 2^-224 and is selected away afterwards, so the
-                    // loop has no branch (a conditional sqrt was compiled as an exec-mask branch)
-                    double h;
-                    const double r = fast_sqrt(__builtin_fmax(ss, 0x1p-224), h);
-                    dist = ss == 0.0 ? 0.0 : r;
+                    dist = fast_dist<SEL>(ss);
                 } else {
                     dist = __builtin_sqrt(ss);
                 }
@@ -449,10 +459,11 @@ __global__ void dist_reduce_kernel(const double* part, int64_t na, int K, double
 }
 
 // st_tune key 13: energy kernel variant (0 / -1 auto; 1: one partial sum, 4 blocks per CU -- round 2;
-// 2: U = 2, 4 blocks; 3: U = 1, 8 blocks; 4: U = 2, 8 blocks; 5: U = 4, 4 blocks)
+// 2: U = 2, 4 blocks; 3: U = 1, 8 blocks; 4: U = 2, 8 blocks; 5: U = 4, 4 blocks;
+// 6: variant 1 with the round-2 zero-distance select, SEL)
 static int g_dist_variant = 0;
 int dist_tune(int value) {
-    if (value < -1 || value > 5) return -1;
+    if (value < -1 || value > 6) return -1;
     g_dist_variant = value < 0 ? 0 : value;
     return 0;
 }
@@ -464,6 +475,7 @@ static void launch_dist_ct(const DistArgs& p, dim3 grid, hipStream_t s) {
         case 3: dist_colsum_kernel<D, 1, 8><<<grid, kColBlock, 0, s>>>(p); break;
         case 4: dist_colsum_kernel<D, 2, 8><<<grid, kColBlock, 0, s>>>(p); break;
         case 5: dist_colsum_kernel<D, 4, 4><<<grid, kColBlock, 0, s>>>(p); break;
+        case 6: dist_colsum_kernel<D, 1, 4, true><<<grid, kColBlock, 0, s>>>(p); break;
         default: dist_colsum_kernel<D, 1, 4><<<grid, kColBlock, 0, s>>>(p); break;
     }
 }
