@@ -72,7 +72,10 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * oracle/stein_ref.c and DESIGN.md §3; all ranks of a sharded run must use the same value), key 12 =
  * register rows per thread of the one-device compact-only persistent kernel (8 .. 10; 0 = do not use
  * it; -1 = automatic: 9, or 10 when more than 2048 rows per block would still be streamed; fewer
- * when a block has fewer rows).
+ * when a block has fewer rows), key 13 = energy-distance kernel variant (0 / -1 = automatic = 1:
+ * one partial sum per thread, 4 blocks per CU; 2..5: more partial sums or 8 blocks per CU; 6: the
+ * round-2 zero-distance select -- measured alternatives; same distances, sums within
+ * rounding).
  */
 int st_tune(int32_t key, int32_t value);
 
