@@ -54,11 +54,11 @@ CHAIN_LEN = 200_000
 RW_STEP = 0.0052   # acceptance ~0.23 as the reference RW-MH chains (Sampling.ipynb cell 28)
 
 
-def lv_surrogate(n: int, seed: int):
+def lv_surrogate(n: int, seed: int, chain_len: int = CHAIN_LEN):
     """Pooled seeded RW-MH chains on N(LV_MEAN, LV_COV) -> (x, grad log p, log p, (log q, grad log q))."""
     from scipy.stats import multivariate_normal as mvn
     rng = np.random.default_rng(seed)
-    chains = max(1, (n + CHAIN_LEN - 1) // CHAIN_LEN)
+    chains = max(1, (n + chain_len - 1) // chain_len)
     steps = (n + chains - 1) // chains
     prec = np.linalg.inv(LV_COV)
     d = LV_MEAN.shape[0]
@@ -88,6 +88,25 @@ def lv_surrogate(n: int, seed: int):
     return x, grad, log_p, (log_q, grad_q)
 
 
+def lv_call_shape(n: int, seed: int, shape: str):
+    """The reference's own LV thinning calls on one RW-MH chain (Stein_thinning.ipynb cells 12, 14;
+    n ~ 5e5 per chain, Sampling.ipynb cells 16-18): the chain lives on the log-parameters s and the
+    gradients on theta = exp(s), so
+      shape 'exp': thin(np.exp(s), grads, 10_000, preconditioner='med')          (json :204)
+      shape 'log': thin(s, np.exp(s) * grads, 10_000, preconditioner='med')     (json :264)
+    Surrogate: s = one RW-MH chain on N(LV_MEAN, LV_COV) (log space) and grads = d log p / d theta =
+    (d log p / d s) / theta (the log-space score divided by the chain rule's factor).  Returns the
+    (sample, gradient) pair the call passes."""
+    s, gs, _, _ = lv_surrogate(n, seed, chain_len=n)
+    theta = np.exp(s)
+    grads = gs / theta
+    if shape == 'exp':
+        return theta, grads
+    if shape == 'log':
+        return s, np.exp(s) * grads
+    raise ValueError(shape)
+
+
 def gaussian_d50(n: int, seed: int, d: int = 50, rho: float = 0.5):
     """Config 5: iid N(0, AR(1) rho) in d=50; gradient-free with q = N(mean, 1.2 cov)."""
     from scipy.stats import multivariate_normal as mvn
@@ -108,6 +127,11 @@ CONFIGS = {
     'c4': dict(desc='LV-surrogate pooled d=4 n=2e6 Langevin IMQ med m=1000', n=2_000_000, m=1000, gf=False, seed=12345),
     'c5': dict(desc='Gaussian AR(1) d=50 n=5e5 gradient-free IMQ med m=500', n=500_000, m=500, gf=True, seed=12349,
                d50=True),
+    # the reference's LV call (not a BASELINE config): one chain of 5e5, m = 10 000, 'med'
+    'lv': dict(desc="LV call shape: thin(np.exp(s), grads, 10_000, 'med') on one RW-MH chain n=5e5 "
+                    "(Stein_thinning.ipynb:204)", n=500_000, m=10_000, gf=False, seed=12350, lv_shape='exp'),
+    'lvlog': dict(desc="LV call shape, log space: thin(s, np.exp(s) * grads, 10_000, 'med'), n=5e5 "
+                       "(Stein_thinning.ipynb:264)", n=500_000, m=10_000, gf=False, seed=12350, lv_shape='log'),
 }
 
 
@@ -143,6 +167,9 @@ def make_integrand(cfg):
         with warnings.catch_warnings():
             warnings.simplefilter('ignore')
             return st._make_stein_gf_integrand(x, log_p, log_q, gq, preconditioner='med'), x, None
+    if cfg.get('lv_shape'):
+        x, g = lv_call_shape(cfg['n'], cfg['seed'], cfg['lv_shape'])
+        return st._make_stein_integrand(x, g, preconditioner='med'), x, g
     x, g, log_p, (log_q, gq) = lv_surrogate(cfg['n'], cfg['seed'])
     if cfg['gf']:
         with warnings.catch_warnings():
@@ -179,7 +206,10 @@ def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None, arith='compact'):
     pairs = cfg['n'] * (steps + 1)
     full = cfg['n'] * cfg['m']
     host = f"{platform.processor() or platform.machine()} ({os.cpu_count()} logical CPUs visible)"
-    return {'value': full / dt_c, 'unit': 'pair-evals/s', 'cores': nt, 'kind': 'port',
+    share = ('the box\'s CPU share for its one GPU: the pool sets OMP_NUM_THREADS=16 and allows '
+             '16 CPUs per GPU, while os.cpu_count() reports the whole host' if os.environ.get('OMP_NUM_THREADS') == '16'
+             else f'OMP_NUM_THREADS / os.cpu_count() on this host')
+    return {'value': full / dt_c, 'unit': 'pair-evals/s', 'cores': nt, 'cores_reason': share, 'kind': 'port',
             'sample': (f"oracle/stein_ref.c sr_greedy_mt (C restatement of the reference greedy loop, "
                        f"JAX_Stein_Thinning.ipynb:281-295, bit model of the kernels, {arith} arithmetic) on {nt} host "
                        f"threads: the full "
@@ -307,6 +337,8 @@ def main():
     ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
     ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
     ap.add_argument('--energy-variant', type=int, default=0, help='energy kernel (st_tune key 13; 0 = auto)')
+    ap.add_argument('--energy-units', type=int, default=-1,
+                    help='energy kernel work units per launch (st_tune key 14; -1 = auto)')
     ap.add_argument('--arith', default='compact', choices=['compact', 'exact'],
                     help='arithmetic of the d <= 8 greedy kernels (stein_thinning.set_arithmetic)')
     ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks'],
@@ -428,9 +460,12 @@ def main():
             alg_bytes = int(pairs_launch * bytes_per_pair)
             rec = pmc_rec.get(f'{args.config}_persistent') if world == 1 else None
             traffic = round(rec['hbm_bytes_per_launch']) if rec else None
+            traffic_src = (f"profiles/pmc_traffic.json['{args.config}_persistent']: {rec.get('source', 'rocprofv3 --pmc pass')}"
+                           f" of {rec['kernel']} (FETCH_SIZE / WRITE_SIZE, gfx950 corrections) -- a committed "
+                           f"measurement of this workload, not taken in this run") if rec else None
             roofline = {
                 'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
-                'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': traffic,
+                'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'traffic': traffic, 'traffic_source': traffic_src,
                 'kernel': _persistent_label(n // world, d, gf, arithmetic, world)
                           + (f' x{world} ranks' if sharded else ''),
                 'kernel_median_us': round(med * 1e6, 1), 'kernel_avg_us': round(avg * 1e6, 1),
@@ -446,9 +481,14 @@ def main():
                          '(PMC traffic per launch = "traffic", far below the streaming figure), so the roofline is '
                          'fp64 VALU (MI355X fp64 vector peak 78.6 TF = fp64 matrix peak; no MFMA shape fits '
                          'the per-pair scalar work); part of each step is the in-launch winner exchange'),
-                'hbm_view': {'algorithmic_bytes_per_launch': alg_bytes, 'bytes_per_pair': bytes_per_pair,
-                             'achieved_GBs': round(alg_bytes / med / 1e9, 1), 'peak_GBs': HBM_PEAK_GBS,
-                             'frac': round(alg_bytes / med / 1e9 / HBM_PEAK_GBS, 4)},
+                'hbm_view': {'measured_bytes_per_launch': traffic,
+                             'measured_GBs': round(traffic / med / 1e9, 1) if traffic else None,
+                             'peak_GBs': HBM_PEAK_GBS,
+                             'measured_frac': round(traffic / med / 1e9 / HBM_PEAK_GBS, 4) if traffic else None,
+                             'streaming_design_bytes_per_launch': alg_bytes, 'bytes_per_pair': bytes_per_pair,
+                             'note': 'HBM is not the bound: the rows stay on chip, so the kernel moves the measured '
+                                     'bytes, not the streaming design\'s n m (16 d + 16) B (SURVEY 8(d)), which '
+                                     'would exceed HBM peak at this kernel time'},
             }
         if not sharded and not args.no_kernel_timing:
             s_avg, s_med = kernel_timing(prob, min(m, 200))
@@ -532,12 +572,19 @@ def main():
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic (seeded RW-MH LV-surrogate chains; see bench.py docstring)',
-            'config': {'workload': f"config {args.config[1]}: {cfg['desc']}", 'n': n, 'd': d, 'm': m,
+            'config': {'workload': (f"config {args.config[1]}: {cfg['desc']}" if args.config[0] == 'c' else cfg['desc']),
+                       'n': n, 'd': d, 'm': m,
                        'preconditioner': 'med', 'kernel': 'gradient-free' if integrand.weights is not None else 'langevin',
                        'parallelism': (f'rows-sharded x{world}, per-step exchange: {runner.mode}'
                                        if sharded else 'single-gpu'),
                        'arithmetic': arithmetic if d <= 8 else 'exact',
-                       'wallclock_thin_s': elapsed / args.steps,
+                       'wallclock_thin_s': {
+                           'device_resident': elapsed / args.steps,
+                           'thin_host_arrays': e2e['thin_host_arrays_s'] if rank == 0 and e2e else None,
+                           'note': 'device_resident = ms_per_step: the timed thin of the standardised sample '
+                                   'already in HBM (value); thin_host_arrays = the drop-in thin(sample, gradient, '
+                                   'm) on host NumPy arrays (validation, standardisation, med, H2D, launch, D2H), '
+                                   'timed once after the timed region'},
                        'first_indices': result_idx[:8].tolist()},
             'exchange': exchange,
             'degraded': degraded,
@@ -583,6 +630,7 @@ def main_energy(args):
     # the selection's triangle
     from stein_thinning import _native as nat
     nat.check(nat.lib().st_tune(13, args.energy_variant), 'st_tune')
+    nat.check(nat.lib().st_tune(14, args.energy_units), 'st_tune')
     curve = se.EnergyCurve(validation, x[idx], cache_reference=False)
     pairs = curve.pair_count()
     curve_c = se.EnergyCurve(validation, x[idx])
@@ -640,7 +688,7 @@ def main_energy(args):
             'roofline': {'bound': 'valu', 'achieved': round(tflops, 2), 'peak': FP64_VALU_PEAK_TFS, 'unit': 'TFLOP/s',
                          'frac': round(tflops / FP64_VALU_PEAK_TFS, 4),
                          'traffic': pmc_traffic('energy') if world == 1 else None,
-                         'kernel': f'dist_colsum_kernel<{d},U,MINB> variant {args.energy_variant} (+ reduce / cumsum)', 'step_median_us': round(step_s * 1e6, 1),
+                         'kernel': f'dist_colsum_kernel<{d},U,MINB> variant {args.energy_variant} units {args.energy_units} (+ reduce / cumsum)', 'step_median_us': round(step_s * 1e6, 1),
                          'flop_per_pair': flop_pair,
                          'note': 'per pair: d differences, squares and sums, one correctly rounded sqrt (the '
                                  'range-guarded ~10-instruction sequence, one quarter-rate v_rsq_f64) and the '

@@ -45,7 +45,9 @@ int check_problem(const double* x, const double* g, const double* w, int64_t n, 
 // workspace layout: [control block (persistent kernel counters/status)][two ping-pong banks of
 // per-block candidate records, kMaxBlocks x stride doubles each]
 int64_t greedy_ws_bytes(int32_t d) {
-    return st::kWsControlBytes + 2 * (int64_t)st::kMaxBlocks * st::cand_stride(d) * 8;
+    const int64_t steps = st::kWsControlBytes + 2 * (int64_t)st::kMaxBlocks * st::cand_stride(d) * 8;
+    const int64_t persist = st::persistent_ws_max_bytes();
+    return steps > persist ? steps : persist;
 }
 
 double* bank(void* ws, int32_t d, int b) {
@@ -82,7 +84,9 @@ int st_tune(int32_t key, int32_t value) {
     int rc;
     if (key == 7) rc = st::proxy_tune(value);
     else if (key == 13) rc = st::dist_tune(value);
-    else rc = ((key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12) ? st::persistent_tune(key, value)
+    else if (key == 14) rc = st::dist_units_tune(value);
+    else rc = ((key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12 || key == 15)
+                  ? st::persistent_tune(key, value)
                                                                                           : st::tune(key, value);
     if (rc != 0) return fail(ST_ERR_INVALID, "bad tuning key/value %d=%d", key, value);
     return ST_OK;

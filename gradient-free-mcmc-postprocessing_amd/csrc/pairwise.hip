@@ -92,8 +92,9 @@ __global__ __launch_bounds__(256) void kmat_kernel(PairArgs p, int64_t k, double
 // as block-uniform broadcasts; 4 blocks (16 waves) per CU; block b takes column block NB-1-b so
 // the heavy (late) columns are dispatched first.  Per pair: the compact arithmetic (st_tune key 11,
 // the default; stein_math.hpp pair_compact_ct) when the block's columns and the staged rows are all
-// in range, else the bits of pair_value_ct (the range-guarded fast form when they admit it: the
-// exact setting); per column: a sequential sum in increasing a.
+// in range; in other tiles the same setting decides per pair (pair_value_sel), so a row shard's
+// bounds never change a pair's bits; the exact setting takes pair_value_ct (the range-guarded fast
+// form when the tile admits it); per column: a sequential sum in increasing a.
 // ------------------------------------------------------------------------------------------
 constexpr int kColBlock = 256;
 constexpr int kColsumUnroll = 2;   // rows per iteration of the column-sum sweep
@@ -131,6 +132,7 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
     }
     const double wi = (GF && live) ? p.w[i] : 1.0;
     const double l = p.l, l2 = p.l * p.l, m3l2 = -3.0 * l2, tr = p.tr;
+    const bool col_ok = cok != 0;   // this column (and l, tr) in range: the per-pair rule's column half
     const int col_fast = __syncthreads_and(cok);
     const int64_t a_stop = p.a1 < c0 + R ? p.a1 : c0 + R;   // rows a < i <= c0 + R - 1
     double acc = 0.0;
@@ -153,7 +155,10 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
         // every row of a tile that ends at or before the block's first column precedes all its
         // columns: no per-pair triangle predicate (only the diagonal tile keeps it)
         const bool below = ac + cnt <= c0;
-        // AR: 0 exact general, 1 exact range-guarded (same bits), 2 compact
+        // AR: 0 exact general, 1 exact range-guarded (same bits), 2 compact, 3 compact per pair
+        // (stein_math.hpp pair_value_sel: compact iff the column and the row are in range, else exact
+        // general) -- a tile with some row or column out of range under the compact setting, so a
+        // pair's bits never depend on which tile (or which rank's row shard) it falls in
         auto sweep = [&](auto ar_tag, auto below_tag) {
             constexpr int AR = decltype(ar_tag)::value;
             constexpr bool BELOW = decltype(below_tag)::value;
@@ -164,6 +169,8 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
                 for (int k = 0; k < D; ++k) { xa[k] = sx[k][e]; ga[k] = sg[k][e]; }
                 double kv;
                 if constexpr (AR == 2) kv = pair_compact_ct<D>(xi, gi, xa, ga, l, m3l2, tr);
+                else if constexpr (AR == 3)
+                    kv = pair_value_sel<D>(col_ok && row_in_range<D>(xa, ga), xi, gi, xa, ga, l, l2, m3l2, tr);
                 else kv = pair_value_ct<D, AR == 1>(xi, gi, xa, ga, l, l2, tr);
                 if constexpr (GF) kv = (kv * wi) * sw[e];
                 return kv;
@@ -190,9 +197,13 @@ __global__ __launch_bounds__(kColBlock, 4) void ksd_colsum_kernel(ColsumArgs p) 
         using C0 = std::integral_constant<int, 0>;
         using C1 = std::integral_constant<int, 1>;
         using C2 = std::integral_constant<int, 2>;
+        using C3 = std::integral_constant<int, 3>;
         if (fast && p.compact) {
             if (below) sweep(C2{}, std::true_type{});
             else sweep(C2{}, std::false_type{});
+        } else if (p.compact) {
+            if (below) sweep(C3{}, std::true_type{});
+            else sweep(C3{}, std::false_type{});
         } else if (fast) {
             if (below) sweep(C1{}, std::true_type{});
             else sweep(C1{}, std::false_type{});
@@ -480,13 +491,25 @@ static void launch_dist_ct(const DistArgs& p, dim3 grid, hipStream_t s) {
     }
 }
 
-// B chunks per launch: enough blocks to fill the chip (>= 2048 over both grid dimensions) without
-// chunks shorter than four staging tiles (1024 points)
+// B chunks per launch: enough (block, chunk) work units that the chip's 1024 resident blocks take
+// many rounds of them, so the last round's imbalance is a small share of the launch, without chunks
+// shorter than four staging tiles (1024 points).  Round 3 aimed at 2 048 units: the 2e5-point
+// validation triangle then had ~1 170 equal full-chunk units for 1 024 slots -- two rounds, the
+// second 14 % full (PMC: ~3 waves per SIMD on average, profiles/r04_energy_stall.json).  Same box,
+// alternating (profiles/r04_energy_units_ab.log): 2 048 -> 22.5 ms per uncached curve, 8 192 -> 19.1,
+// 16 384 -> 17.5, 32 768 -> 16.9 (0.148 -> 0.198 of fp64 peak); st_tune key 14 sets the target (grid
+// blocks over both dimensions).
+static int64_t g_dist_units = 32768;
+int dist_units_tune(int value) {
+    if (value != -1 && (value < 256 || value > (1 << 22))) return -1;
+    g_dist_units = value < 0 ? 32768 : value;
+    return 0;
+}
 int64_t distance_chunks(int64_t na, int64_t b_begin, int64_t b_end) {
     const int64_t ablocks = (na + kColBlock - 1) / kColBlock;
     const int64_t range = b_end - b_begin;
     if (ablocks <= 0 || range <= 0) return 1;
-    int64_t K = (2048 + ablocks - 1) / ablocks;
+    int64_t K = (g_dist_units + ablocks - 1) / ablocks;
     const int64_t kmax = (range + 4 * kColBlock - 1) / (4 * kColBlock);
     if (K > kmax) K = kmax;
     if (K > 65535) K = 65535;

@@ -192,6 +192,7 @@ struct PersistArgs {
     const unsigned* gate; // general kernel after a compact-only one: run only if *gate == 2
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
+    int stream_a_lds;     // 512-thread kernels: the streamed rows' running sums are kept in LDS
     uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
     int rec_stride;               // record pitch in granules (2 = packed; wider spreads the polled
                                   // records over more memory channels)
@@ -673,6 +674,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     double* const srow0 = lds + (sizeof(Scratch) + 15) / 16 * 2;
     auto lrow = [&](int e) -> double* { return srow0 + (e >> 6) * (kLF * 64) + (e & 63); };
     constexpr int fX = 0, fG = D * 64, fA = 2 * D * 64, fW = (2 * D + 1) * 64;   // field offsets
+    // 512-thread kernels with st_tune key 15 = 1: the streamed rows' running sums live in LDS too,
+    // after the LDS rows (one double per streamed row, whole 64-row chunks), so a streamed row is
+    // read-only L2 traffic -- no per-step load and store of A (measured slower: see key 15)
+    double* const sA = srow0 + (int64_t)(RL >> 6) * (kLF * 64);
     const int tid = threadIdx.x;
     const int64_t ld = a.ld;
     const int64_t r0 = a.row_begin + (int64_t)blockIdx.x * a.rows_per_block;
@@ -766,7 +771,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             for (int k = 0; k < D; ++k) { gi[k] = a.g[k * ld + row]; xi[k] = a.x[k * ld + row]; }
             double kv = CMP ? diag_value_sel<D>(lok && row_in_range<D>(xi, gi), gi, tr) : diag_value_ct<D>(gi, tr);
             if constexpr (GF) kv = (kv * a.w[row]) * a.w[row];
-            a.A[row] = kv;
+            if (kDyn && a.stream_a_lds) sA[row - str_base] = kv;
+            else a.A[row] = kv;
             scan_take(kv, (uint32_t)row, bv, bi);
         }
     }
@@ -907,12 +913,6 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                         c = __hip_atomic_fetch_add(ctr, 2, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     return __builtin_amdgcn_readfirstlane(c);
                 };
-                // branch-free tail handling, so the two streamed chunks of an iteration stay in one
-                // basic block with all their loads issued up front: rows past r1 store through a
-                // buffer descriptor that ends at r1 (dropped by the range check) and scan as +inf
-                // with the largest index
-                const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(
-                    a.A + str_base, 0, ns > 0 ? (int)(ns * 8) : 0, 0x00020000);
                 // streamed rows through descriptors based at str_base: ONE 32-bit lane offset per
                 // row, the column offsets k * ld * 8 as SGPR operands (no 64-bit address per
                 // coordinate; the host keeps (d - 1) * ld * 8 + rows * 8 below 2^31).  Rows past r1
@@ -923,54 +923,72 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                                                                    0x7FFFFFFF, 0x00020000);
                 const auto wrs = __builtin_amdgcn_make_buffer_rsrc(
                     const_cast<double*>(GF ? a.w + str_base : a.x), 0, 0x7FFFFFFF, 0x00020000);
-                auto fetch = [&](int64_t row, SRow& r) {
-                    const int off = row < r1 ? (int)((row - str_base) * 8) : 0;
+                // SAL: the streamed rows' sums in LDS (sA; the host's choice whenever they fit next to
+                // the LDS rows) -- else in HBM through a descriptor that ends at r1.  Branch-free
+                // tail handling either way, so the two streamed chunks of an iteration stay in one
+                // basic block with all their loads issued up front: rows past r1 (the last chunk's
+                // tail) keep their garbage sum in the chunk's unused LDS slots or store past the
+                // descriptor's range (dropped), and scan as +inf with the largest index
+                auto chunk_loop = [&](auto sal_tag) {
+                    constexpr bool SAL = decltype(sal_tag)::value;
+                    const auto arsrc = __builtin_amdgcn_make_buffer_rsrc(
+                        a.A + str_base, 0, (!SAL && ns > 0) ? (int)(ns * 8) : 0, 0x00020000);
+                    auto fetch = [&](int64_t row, SRow& r) {
+                        const int off = row < r1 ? (int)((row - str_base) * 8) : 0;
 #pragma unroll
-                    for (int k = 0; k < D; ++k) {
-                        r.x[k] = buf_load_f64(xrs, off, (int)(k * ld * 8));
-                        r.g[k] = buf_load_f64(grs, off, (int)(k * ld * 8));
+                        for (int k = 0; k < D; ++k) {
+                            r.x[k] = buf_load_f64(xrs, off, (int)(k * ld * 8));
+                            r.g[k] = buf_load_f64(grs, off, (int)(k * ld * 8));
+                        }
+                        if constexpr (SAL) r.a = sA[row - str_base];
+                        else r.a = buf_load_f64(arsrc, off, 0);
+                        r.w = GF ? buf_load_f64(wrs, off, 0) : 1.0;
+                    };
+                    auto take_stream = [&](int64_t row, double av) {
+                        const bool in = row < r1;
+                        if constexpr (SAL) {
+                            sA[row - str_base] = av;
+                        } else {
+                            typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                            const uint64_t ab = (uint64_t)__double_as_longlong(av);
+                            __builtin_amdgcn_raw_buffer_store_b64(u32x2{(unsigned)ab, (unsigned)(ab >> 32)}, arsrc,
+                                                                  in ? (int)((row - str_base) * 8) : (int)(ns * 8), 0, 0);
+                        }
+                        scan_take_idx<FAST>(in ? av : INFINITY, in ? (uint32_t)row : 0xFFFFFFFFu, bv, bi);
+                    };
+                    auto one_chunk = [&](int c) {
+                        if (c < nS) {
+                            const int64_t s0 = str_base + ((int64_t)c << 6) + lane;
+                            SRow ra;
+                            fetch(s0, ra);
+                            take_stream(s0, stream_pair(ra));
+                        } else {
+                            const int e0 = ((c - nS) << 6) + lane;
+                            scan_take_idx<FAST>(lds_pair(e0), (uint32_t)(lds_base + e0), bv, bi);
+                        }
+                    };
+                    for (int c = grab(); c < nC; c = grab()) {
+                        if (c + 1 < nS) {            // two streamed chunks: both loads in flight
+                            const int64_t s0 = str_base + ((int64_t)c << 6) + lane, s1 = s0 + 64;
+                            SRow ra, rb;
+                            fetch(s0, ra);
+                            fetch(s1, rb);
+                            const double av0 = stream_pair(ra), av1 = stream_pair(rb);
+                            take_stream(s0, av0);
+                            take_stream(s1, av1);
+                        } else if (c >= nS && c + 1 < nC) {   // two LDS chunks: two chains
+                            const int e0 = ((c - nS) << 6) + lane, e1 = e0 + 64;
+                            const double av0 = lds_pair(e0), av1 = lds_pair(e1);
+                            scan_take_idx<FAST>(av0, (uint32_t)(lds_base + e0), bv, bi);
+                            scan_take_idx<FAST>(av1, (uint32_t)(lds_base + e1), bv, bi);
+                        } else {                     // the stream/LDS seam or the last chunk
+                            one_chunk(c);
+                            if (c + 1 < nC) one_chunk(c + 1);
+                        }
                     }
-                    r.a = buf_load_f64(arsrc, off, 0);
-                    r.w = GF ? buf_load_f64(wrs, off, 0) : 1.0;
                 };
-                auto take_stream = [&](int64_t row, double av) {
-                    const bool in = row < r1;
-                    typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
-                    const uint64_t ab = (uint64_t)__double_as_longlong(av);
-                    __builtin_amdgcn_raw_buffer_store_b64(u32x2{(unsigned)ab, (unsigned)(ab >> 32)}, arsrc,
-                                                          in ? (int)((row - str_base) * 8) : (int)(ns * 8), 0, 0);
-                    scan_take_idx<FAST>(in ? av : INFINITY, in ? (uint32_t)row : 0xFFFFFFFFu, bv, bi);
-                };
-                auto one_chunk = [&](int c) {
-                    if (c < nS) {
-                        const int64_t s0 = str_base + ((int64_t)c << 6) + lane;
-                        SRow ra;
-                        fetch(s0, ra);
-                        take_stream(s0, stream_pair(ra));
-                    } else {
-                        const int e0 = ((c - nS) << 6) + lane;
-                        scan_take_idx<FAST>(lds_pair(e0), (uint32_t)(lds_base + e0), bv, bi);
-                    }
-                };
-                for (int c = grab(); c < nC; c = grab()) {
-                    if (c + 1 < nS) {            // two streamed chunks: both loads in flight
-                        const int64_t s0 = str_base + ((int64_t)c << 6) + lane, s1 = s0 + 64;
-                        SRow ra, rb;
-                        fetch(s0, ra);
-                        fetch(s1, rb);
-                        const double av0 = stream_pair(ra), av1 = stream_pair(rb);
-                        take_stream(s0, av0);
-                        take_stream(s1, av1);
-                    } else if (c >= nS && c + 1 < nC) {   // two LDS chunks: two chains
-                        const int e0 = ((c - nS) << 6) + lane, e1 = e0 + 64;
-                        const double av0 = lds_pair(e0), av1 = lds_pair(e1);
-                        scan_take_idx<FAST>(av0, (uint32_t)(lds_base + e0), bv, bi);
-                        scan_take_idx<FAST>(av1, (uint32_t)(lds_base + e1), bv, bi);
-                    } else {                     // the stream/LDS seam or the last chunk
-                        one_chunk(c);
-                        if (c + 1 < nC) one_chunk(c + 1);
-                    }
-                }
+                if (a.stream_a_lds) chunk_loop(std::true_type{});
+                else chunk_loop(std::false_type{});
                 ST_STAMP_AFTER(a, t, 6, bv);
             } else {
                 // (two waves per SIMD: two chains per wave are enough and leave room for the rows)
@@ -1052,6 +1070,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
         const int64_t row = lds_base + e;
         if (row < r1) a.A[row] = lrow(e)[fA];
     }
+    if (kDyn && a.stream_a_lds)
+        for (int64_t row = str_base + tid; row < r1; row += kPBlock) a.A[row] = sA[row - str_base];
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1064,10 +1084,22 @@ int64_t persistent_rep_stride(int G, int rec_stride, int nrep) {
     return nrep == 1 ? one : (one + 63) / 64 * 64 + 32;
 }
 
+// one kernel's record region: 2 banks x nrep replicas x G records
+static int64_t persistent_region_bytes(int G, int rec_stride, int nrep) {
+    return 2 * (int64_t)nrep * persistent_rep_stride(G, rec_stride, nrep) * 8;
+}
+
 int64_t persistent_ws_bytes(int d, int G, int rec_stride, int nrep) {
-    // [control: status (and reserved) words][2 banks x nrep replicas x G records]
+    // [control: status (and reserved) words][record region][record region of the general kernel
+    // behind a compact-only run, when the workspace holds it]
     (void)d;
-    return kWsControlBytes + 2 * (int64_t)nrep * persistent_rep_stride(G, rec_stride, nrep) * 8;
+    return kWsControlBytes + persistent_region_bytes(G, rec_stride, nrep);
+}
+
+// workspace the persistent launcher can use at most: two record regions (compact-only kernel and
+// the general kernel gated behind it) at the widest grid, default replicas and packed records
+int64_t persistent_ws_max_bytes() {
+    return kWsControlBytes + 2 * persistent_region_bytes(kMaxGrid, kRecGranules, kDefaultRecReplicas);
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
@@ -1077,6 +1109,12 @@ static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
 static int g_persist_pitch = -1; // st_tune key 9: record pitch in bytes (16 .. 4096, power of 2), -1 auto
 static int g_persist_nrep = -1;  // st_tune key 10: record replicas (1 .. 32, power of 2), -1 auto
 static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register rows (8 .. 10), 0 off, -1 auto
+// st_tune key 15: the 512-thread kernels keep the streamed rows' running sums in LDS (1) or in HBM (0,
+// the default).  Measured (round 4, same box, config 4, profiles/r04_streamed_sums_lds_rejected.log):
+// PMC WRITE_SIZE 1.08 GB -> 0.15 GB per thin, but 6.82 -> 6.94-7.01 ms: the 8 B per streamed row take
+// LDS from ~120 LDS rows, which then stream (~1.1 ns instead of ~0.36 ns per row-step), and the A
+// load / store it saves was not on the critical path (L2-resident, stores fire-and-forget).
+static int g_persist_sal = 0;
 // automatic register rows of the compact-only kernel: 9 (28 B of scratch at d = 4) unless more than
 // kCmpStreamRows rows per block would still be streamed, then 10 (108 B of scratch; the streamed
 // rows then no longer stay in the XCD's L2).  Same-box, d = 4, m = 1000 (profiles/r03_compact_only_rt.log):
@@ -1121,6 +1159,11 @@ int persistent_tune(int key, int value) {
     if (key == 12) {
         if (value != -1 && value != 0 && (value < 8 || value > 10)) return -1;
         g_persist_cmp = value;
+        return 0;
+    }
+    if (key == 15) {
+        if (value < -1 || value > 1) return -1;
+        g_persist_sal = value < 0 ? 0 : value;
         return 0;
     }
     return -1;
@@ -1244,8 +1287,12 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     if (persistent_ws_bytes(d, G, pitch, nrep) > ws_bytes) return hipErrorNotSupported;
     const int64_t R = (n_shard + G - 1) / G;
     if (wide && R > 256) return hipErrorNotSupported;   // wide: one register row per thread only
-    // streamed rows are addressed with 32-bit buffer offsets (column k at k * ld * 8 bytes)
-    if ((int64_t)(d - 1) * ld * 8 + (R + 64) * 8 >= 0x7FFFFFFFll) return hipErrorNotSupported;
+    // the 512-thread kernels address streamed rows with 32-bit buffer offsets (column k at
+    // k * ld * 8 bytes from the block's first streamed row): only a launch that streams rows needs
+    // them below 2^31 (the 256-thread and wide kernels use 64-bit addresses)
+    auto offsets_ok = [&](int nt_, int rt_, int64_t rl_) {
+        return nt_ != 512 || R <= (int64_t)rt_ * nt_ + rl_ || (int64_t)(d - 1) * ld * 8 + (R + 64) * 8 < 0x7FFFFFFFll;
+    };
     // auto: 512-thread blocks (two waves per SIMD, dynamic chunks) once a block has more rows than
     // one wave per SIMD keeps in registers comfortably (measured crossover 1e3 .. 2e3 rows per CU,
     // scripts/sweep_nt_crossover.sh)
@@ -1261,15 +1308,30 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);
     const size_t head = (sizeof(Scratch) + 15) / 16 * 16;
     const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) / bpc - 1024;   // static + slack
-    int64_t RL = (int64_t)((budget - head) / row_bytes);
-    const int64_t need = R - (int64_t)rt * nt;
-    if (RL > need) RL = need > 0 ? need : 0;
-    RL = RL / 64 * 64;
-    if (RL < 0) RL = 0;
-    if (wide) RL = 0;
+    // LDS rows (whole 64-row chunks) for rows past the register rows; the 512-thread (dynamic-chunk)
+    // kernels also keep every streamed row's running sum in LDS (8 B per row, whole chunks)
+    // (st_tune key 15 = 1 only; when the streamed sums alone would not fit -- more than ~20 000
+    // streamed rows per block -- they stay in HBM: sal = 0)
+    auto lds_rows = [&](int nt_, int rt_, int64_t& rl, size_t& bytes, int& sal) {
+        const int64_t need_ = R - (int64_t)rt_ * nt_;
+        sal = g_persist_sal == 1 && nt_ == 512 && bpc == 1 && need_ > 0 &&
+              head + (size_t)(need_ + 63) / 64 * 64 * sizeof(double) <= budget;
+        rl = need_ > 0 ? need_ / 64 * 64 : 0;
+        auto total = [&](int64_t l) {
+            const int64_t st = need_ - l > 0 ? (need_ - l + 63) / 64 * 64 : 0;
+            return head + (size_t)l * row_bytes + (sal ? (size_t)st * sizeof(double) : 0);
+        };
+        while (rl > 0 && total(rl) > budget) rl -= 64;
+        bytes = total(rl);
+    };
+    int64_t RL = 0;
+    size_t lds_rows_bytes = head;
+    int sal = 0;
+    if (!wide) lds_rows(nt, rt, RL, lds_rows_bytes, sal);
     // wide: the rows' g lives in LDS (d x 256 doubles: 100 KB at d = 50)
-    const size_t lds = wide ? head + (size_t)d * 256 * sizeof(double) : head + (size_t)RL * row_bytes;
+    const size_t lds = wide ? head + (size_t)d * 256 * sizeof(double) : lds_rows_bytes;
     if (wide && lds > (size_t)(lds_max > 0 ? lds_max : 65536)) return hipErrorNotSupported;
+    if (!wide && !offsets_ok(nt, rt, RL)) return hipErrorNotSupported;
 
     char* p = static_cast<char*>(ws);
     PersistArgs a{};
@@ -1285,6 +1347,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.gran = reinterpret_cast<uint64_t*>(p + kWsControlBytes);
     a.rows_per_block = R;
     a.RL = (int)RL;
+    a.stream_a_lds = sal;
     a.rec_stride = pitch;
     a.nrep = nrep;
     a.rep_stride = persistent_rep_stride(G, pitch, nrep);
@@ -1309,22 +1372,33 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         const int64_t rl_cap = (int64_t)((budget - head) / row_bytes) / 64 * 64;
         rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R - 9 * 512 - rl_cap > kCmpStreamRows ? 10 : 9);
         while (rt_c > 8 && (int64_t)rt_c * 512 > R) --rt_c;   // no empty register rows
-        int64_t RLc = (int64_t)((budget - head) / row_bytes);
-        const int64_t need_c = R - (int64_t)rt_c * 512;
-        if (RLc > need_c) RLc = need_c > 0 ? need_c : 0;
-        RLc = RLc / 64 * 64;
+        int64_t RLc = 0;
+        int salc = 0;
+        lds_rows(512, rt_c, RLc, lds_c, salc);
         ac.RL = (int)RLc;
-        lds_c = head + (size_t)RLc * row_bytes;
-        use_cmp = launch_cmp(ac, d, gf, rt_c, G, lds_c, s, true) == hipSuccess;   // residency check only
+        ac.stream_a_lds = salc;
+        use_cmp = offsets_ok(512, rt_c, RLc) &&
+                  launch_cmp(ac, d, gf, rt_c, G, lds_c, s, true) == hipSuccess;   // residency check only
     }
+    // The gated general kernel must never see a record of the compact-only run: its tags are 8-bit
+    // (they wrap every 256 steps) and the compact-only kernel may stop at any step.  It gets a
+    // record region of its own when the workspace holds one (st_greedy_workspace_bytes does), else
+    // the shared region is zeroed again between the two launches.
+    const int64_t region = persistent_region_bytes(G, pitch, nrep);
+    const bool own_region = use_cmp && kWsControlBytes + 2 * region <= ws_bytes;
     // zero status and every granule tag (a stale tag from a previous run must never match)
-    hipError_t e = hipMemsetAsync(p, 0, (size_t)persistent_ws_bytes(d, G, pitch, nrep), s);
+    hipError_t e = hipMemsetAsync(p, 0, (size_t)(kWsControlBytes + (own_region ? 2 : 1) * region), s);
     if (e != hipSuccess) return e;
     if (use_cmp) {
         e = launch_cmp(ac, d, gf, rt_c, G, lds_c, s, false);
         if (e != hipSuccess) return e;
         a.gate = ac.status;
         a.status = ac.status + 1;
+        if (own_region) {
+            a.gran = reinterpret_cast<uint64_t*>(p + kWsControlBytes + region);
+        } else if ((e = hipMemsetAsync(p + kWsControlBytes, 0, (size_t)region, s)) != hipSuccess) {
+            return e;
+        }
     }
     e = launch_kind(a, d, wide, gf, rt, nt, bpc, G, lds, s, false);
     if (e == hipSuccess) *used = 1;

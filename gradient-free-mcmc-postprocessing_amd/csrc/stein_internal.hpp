@@ -66,6 +66,7 @@ int arith_compact();
 int tune(int key, int value);
 int persistent_tune(int key, int value);
 int64_t persistent_ws_bytes(int d, int G, int rec_stride, int nrep);
+int64_t persistent_ws_max_bytes();
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
@@ -146,6 +147,7 @@ hipError_t launch_ksd_colsum(const PairArgs& p, int64_t n, int64_t a0, int64_t a
 hipError_t launch_ksd_finish(const PairArgs& p, int64_t n, const double* csum, double* ks,
                              hipStream_t s);
 int64_t distance_chunks(int64_t na, int64_t b_begin, int64_t b_end);
+int dist_units_tune(int value);   // st_tune key 14
 hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, const double* b,
                                   int64_t ldb, int64_t b0, int64_t b1, int d, int tri,
                                   double* out, double* ws, int64_t ws_doubles, hipStream_t s);

@@ -128,12 +128,21 @@ def lib() -> ctypes.CDLL:
                     if mode not in ARITHMETIC:
                         raise ValueError(f'ST_ARITH={mode!r}: expected one of {sorted(ARITHMETIC)}')
                     L.st_tune(11, ARITHMETIC[mode])
+                    global _ARITH
+                    _ARITH = mode
                 _LIB = L
     return _LIB
 
 
 # greedy-kernel arithmetic (st_tune key 11; include/stein_thinning_hip.h)
 ARITHMETIC = {'exact': 0, 'compact': 1}
+_ARITH = 'compact'   # what the loaded library was last told (its default until then)
+
+
+def arithmetic() -> str:
+    """The arithmetic the greedy kernels use now ('compact' or 'exact'; set_arithmetic / ST_ARITH)."""
+    lib()
+    return _ARITH
 
 
 def set_arithmetic(mode: str) -> None:
@@ -148,6 +157,8 @@ def set_arithmetic(mode: str) -> None:
     if mode not in ARITHMETIC:
         raise ValueError(f'arithmetic {mode!r}: expected one of {sorted(ARITHMETIC)}')
     check(lib().st_tune(11, ARITHMETIC[mode]), 'set_arithmetic')
+    global _ARITH
+    _ARITH = mode
 
 
 def check_host(rc: int, what: str = '') -> None:

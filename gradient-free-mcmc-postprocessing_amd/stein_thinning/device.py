@@ -99,10 +99,16 @@ class DeviceProblem:
             self.l, self.tr, 0, int(n_points), int(n_points), nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
             ws.numel() * 8, nat.stream_handle()), 'st_greedy_steps')
 
-    def greedy(self, n_points: int, return_sums: bool = False):
+    def greedy(self, n_points: int, return_sums: bool = False, margins: bool = False):
         """The reference's _greedy_search on the device.  ``self.fallback`` is None when the
         persistent launch completed, else why the run was repeated on the launch-per-step path
-        (its bounded waits expired: the grid was not co-resident next to other work)."""
+        (its bounded waits expired: the grid was not co-resident next to other work).
+        ``margins=True``: (indices, diagnostics.GreedyMargins) -- the same selection with each step's
+        argmin margin against the arithmetic's error band (launch-per-step kernels, one step at a time)."""
+        if margins:
+            from .diagnostics import greedy_margins
+            gm = greedy_margins(self, n_points)
+            return gm.indices, gm
         idx, a, ws = self.greedy_buffers(n_points)
         self.greedy_launch(n_points, idx, a, ws)
         out = idx.cpu().numpy().view(np.uint32).copy()

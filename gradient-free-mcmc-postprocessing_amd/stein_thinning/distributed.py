@@ -571,6 +571,9 @@ def sharded_runner(integrand: SteinIntegrand, n_points: int, group=None, use_gra
     record all-gather.  ``runner.mode`` names the engine; ``runner.launch()`` enqueues a further
     run."""
     rank, world = _world(group)
+    if world > 1 and not _group_same(np.array([nat.ARITHMETIC[nat.arithmetic()]], dtype=np.int64), group):
+        raise ValueError('sharded thin: the ranks use different greedy-kernel arithmetics '
+                         '(stein_thinning.set_arithmetic / ST_ARITH must agree on every rank)')
     engine = exchange_engine(integrand.sample.shape[1], world, integrand.n)
     if engine == 'persistent' and not persistent_supported(integrand, rank, world, n_points, group):
         engine = 'steps'   # e.g. d = 50 with more rows per block than the wide kernel holds
@@ -631,11 +634,13 @@ def _engine_runner(integrand: SteinIntegrand, n_points: int, group, use_graph: b
 
 
 def _problem_digest(integrand: SteinIntegrand, n_points: int) -> np.ndarray:
-    """Cheap fingerprint of a thinning problem: shape, m, preconditioner and 4 096 evenly spaced
-    standardised rows (+ weights).  Ranks running independent thins (different chains) differ."""
+    """Cheap fingerprint of a thinning problem: shape, m, preconditioner, the greedy kernels'
+    arithmetic (a rank that set another one would evaluate its shard by other rules) and 4 096 evenly
+    spaced standardised rows (+ weights).  Ranks running independent thins (different chains) differ."""
     n = integrand.n
     rows = np.linspace(0, n - 1, min(n, 4096)).astype(np.int64)
-    parts = [np.array([n, integrand.sample.shape[1], n_points, integrand.weights is not None], dtype=np.int64),
+    parts = [np.array([n, integrand.sample.shape[1], n_points, integrand.weights is not None,
+                       nat.ARITHMETIC[nat.arithmetic()]], dtype=np.int64),
              np.array([integrand.linv_scale, integrand.linv_trace]),
              integrand.sample[rows], integrand.gradient[rows]]
     if integrand.weights is not None:
@@ -644,15 +649,17 @@ def _problem_digest(integrand: SteinIntegrand, n_points: int) -> np.ndarray:
 
 
 def thin_across_ranks(integrand: SteinIntegrand, n_points: int, group=None) -> np.ndarray:
-    """The drop-in ``thin`` / ``thin_gf`` under a multi-rank launch (``thinning._greedy_search``
-    routes here when torch.distributed is initialised with world > 1): the candidate rows are
-    sharded over the ranks exactly as ``thin_sharded`` does, and every rank returns the
-    single-process indices.  Collective: every rank must call it with the same problem -- checked
-    first; ranks thinning different samples (the reference's per-chain fan-out,
-    ``code/src/utils/parallel.py:48-52``) get a ValueError and should set ST_SHARD_THIN=0."""
+    """The drop-in ``thin`` / ``thin_gf`` under a multi-rank launch that opted in to sharding
+    (``thinning._greedy_search`` routes here when torch.distributed is initialised with world > 1 and
+    set_rank_sharding(True) / ST_SHARD_THIN=1): the candidate rows are sharded over the ranks exactly
+    as ``thin_sharded`` does, and every rank returns the single-process indices.  Collective: every
+    rank must call it with the same problem -- checked first; ranks thinning different samples (the
+    reference's per-chain fan-out, ``code/src/utils/parallel.py:48-52``) get a ValueError and should
+    leave sharding off."""
     if not _group_same(_problem_digest(integrand, n_points), group):
         raise ValueError('thin() under torch.distributed: the ranks hold different problems; '
-                         'set ST_SHARD_THIN=0 to thin independently on every rank')
+                         'leave row sharding off (ST_SHARD_THIN unset / set_rank_sharding(False)) '
+                         'to thin independently on every rank')
     return _thin_sharded_integrand(integrand, n_points, group)
 
 

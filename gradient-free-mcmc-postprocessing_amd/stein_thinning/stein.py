@@ -118,9 +118,6 @@ def _record_rows(integrand: Callable, inner: SteinIntegrand, n: int) -> Optional
     return rows
 
 
-_trace_rows = _record_rows
-
-
 def _device_rows(integrand: Callable, n: int) -> Optional[Tuple[SteinIntegrand, np.ndarray]]:
     if isinstance(integrand, SteinIntegrand):
         inner, rows = integrand, np.arange(n, dtype=np.int64)
@@ -130,15 +127,10 @@ def _device_rows(integrand: Callable, n: int) -> Optional[Tuple[SteinIntegrand, 
     inner = _inner_integrand(integrand)
     if inner is None:
         return None
-    rows = _trace_rows(integrand, inner, n)
+    rows = _record_rows(integrand, inner, n)
     if rows is None:
         return None
     return inner, rows
-
-
-def _resolve(integrand: Callable) -> Optional[Tuple[SteinIntegrand, Optional[np.ndarray]]]:
-    """Backward-compatible probe: (SteinIntegrand, None) for a SteinIntegrand, else None."""
-    return (integrand, None) if isinstance(integrand, SteinIntegrand) else None
 
 
 def _problem(inner: SteinIntegrand, rows: np.ndarray):

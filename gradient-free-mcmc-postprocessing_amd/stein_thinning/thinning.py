@@ -249,12 +249,26 @@ def _greedy_search_protocol(n_points: int, integrand: Callable) -> np.ndarray:
     return idx
 
 
+_SHARD_THIN: Optional[bool] = None   # set_rank_sharding(); None: the ST_SHARD_THIN environment variable
+
+
+def set_rank_sharding(enabled: Optional[bool]) -> None:
+    """Opt in (True) or out (False) of row sharding for the drop-in ``thin`` / ``thin_gf`` under a
+    multi-rank launch; None returns to the ST_SHARD_THIN environment variable ('1' = on; off by
+    default).  Sharding makes ``thin`` a collective: every rank must call it with the same problem."""
+    global _SHARD_THIN
+    _SHARD_THIN = None if enabled is None else bool(enabled)
+
+
 def _rank_sharding() -> bool:
-    """True when thin / thin_gf run under a multi-rank launch (torch.distributed initialised with
-    more than one rank, e.g. torchrun with one process per GPU) and ST_SHARD_THIN is not '0': the
-    candidate rows are then split across the ranks (every rank must make the same call)."""
+    """True when thin / thin_gf should shard their candidate rows across the ranks: the caller opted
+    in (set_rank_sharding(True) or ST_SHARD_THIN=1) and torch.distributed is initialised with more
+    than one rank (e.g. torchrun, one process per GPU).  Off by default: a sharded thin is a
+    collective, and scripts that thin on one rank only, or a different chain on every rank (the
+    reference's per-chain fan-out, ``code/src/utils/parallel.py:48-52``), must keep every call local."""
     import os
-    if os.environ.get('ST_SHARD_THIN', '1') == '0':
+    enabled = _SHARD_THIN if _SHARD_THIN is not None else os.environ.get('ST_SHARD_THIN', '0') == '1'
+    if not enabled:
         return False
     try:
         import torch.distributed as dist
@@ -267,8 +281,9 @@ def _greedy_search(n_points: int, integrand: Callable) -> np.ndarray:
     """Greedy KSD minimisation (Algorithm 3, report.tex:413-426); returns uint32 indices.
 
     SteinIntegrand -> the whole m-step loop runs on the GPU (one persistent launch, or one fused
-    kernel per step; no host round trip); under a multi-rank launch its rows are sharded across
-    the ranks (stein_thinning.distributed.thin_across_ranks, same indices).  Any other callable ->
+    kernel per step; no host round trip); under a multi-rank launch that opted in
+    (set_rank_sharding / ST_SHARD_THIN=1) its rows are sharded across the ranks
+    (stein_thinning.distributed.thin_across_ranks, same indices).  Any other callable ->
     the reference protocol loop.
     """
     n_points = int(n_points)

@@ -13,7 +13,8 @@
  *     allocates nothing and never synchronises (graph-capturable) -- except the one-time
  *     multi-GPU setup calls st_mailbox_alloc / st_mailbox_free / st_ipc_*, which are synchronous;
  *   - sample / gradient arrays are SoA: element (i, k) of the (n, d) array lives at p[k * ld + i],
- *     ld a multiple of 8 and >= n; per-row arrays (weights, running sums) have ld entries (rows
+ *     ld a multiple of 8 and >= n (the ABI's requirement, checked; the Python shim pads to a
+ *     multiple of 64, one wave's rows, which the kernels do not require); per-row arrays (weights, running sums) have ld entries (rows
  *     n..ld-1 are padding: read, and in the running sums overwritten, never selected);
  *     all device pointers 16-byte aligned;
  *   - the preconditioner is isotropic Gamma^-1 = linv_scale * I ('id', 'med', 'sclmed', float
@@ -75,7 +76,11 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * when a block has fewer rows), key 13 = energy-distance kernel variant (0 / -1 = automatic = 1:
  * one partial sum per thread, 4 blocks per CU; 2..5: more partial sums or 8 blocks per CU; 6: the
  * round-2 zero-distance select -- measured alternatives; same distances, sums within
- * rounding).
+ * rounding), key 14 = energy-distance work units: grid blocks (256 columns x one B chunk) that
+ * st_distance_colsum_ws aims for (256 .. 2^22; -1 = automatic = 32768; the B range is split into
+ * that many / ceil(na / 256) chunks of at least 1024 points -- sums within rounding), key 15 = the
+ * 512-thread persistent kernels keep the streamed rows' running sums in LDS (1) instead of HBM (0 /
+ * -1 = automatic = 0: measured slower; same results).
  */
 int st_tune(int32_t key, int32_t value);
 
@@ -303,8 +308,9 @@ int st_kmat(const double *x_soa, const double *g_soa, const double *weights, int
 int st_distance_colsum(const double *a_soa, int64_t lda, int64_t na, const double *b_soa,
                        int64_t ldb, int64_t nb, int32_t d, int64_t b_begin, int64_t b_end,
                        int32_t triangle, double *out, void *stream);
-/* The same with the B range split over blockIdx.y chunks (>= 2048 blocks in all: a short A -- e.g.
- * the 1 000 selected points against a 2e5-point validation sample -- still fills the chip): the chunk
+/* The same with the B range split over blockIdx.y chunks (~32768 blocks in all, st_tune key 14: a
+ * short A -- e.g. the 1 000 selected points against a 2e5-point validation sample -- still fills
+ * the chip, and a long triangle is dealt to the CUs in many small units): the chunk
  * partials go to `workspace` (st_distance_workspace_bytes(na, b_begin, b_end) bytes, 16-B aligned;
  * 0 means no split) and are summed per point in chunk order (deterministic). */
 int64_t st_distance_workspace_bytes(int64_t na, int64_t b_begin, int64_t b_end);

@@ -2,15 +2,19 @@
 # HBM traffic (rocprofv3 FETCH_SIZE / WRITE_SIZE, one counter per pass, each pass its own run) of
 # every bench workload's dominant kernel; summarised per launch into profiles/pmc_traffic.json by
 # tools/summarize_pmc.py (gfx950 FETCH_SIZE x2 correction).  Any failing pass ends the script.
-#   bash scripts/pmc_workloads.sh [key ...]      keys: energy ksd_c2 proxy_gauss proxy_t lv
+#   bash scripts/pmc_workloads.sh [key ...]      keys: energy ksd_c2 proxy_gauss proxy_t lv c4_persistent
+# PMC_SOURCE (environment) labels the records (round, commit).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 declare -A ARGS=( [energy]="--workload energy" [ksd_c2]="--workload ksd" [proxy_gauss]="--workload proxy"
-                  [proxy_t]="--workload proxy --proxy-kind t" [lv]="--workload lv" )
+                  [proxy_t]="--workload proxy --proxy-kind t" [lv]="--workload lv"
+                  [c4_persistent]="--config c4 --no-kernel-timing" )
 declare -A KERN=( [energy]="dist_colsum_kernel" [ksd_c2]="ksd_colsum_kernel" [proxy_gauss]="proxy_mfma_buf_kernel"
-                  [proxy_t]="proxy_mfma_buf_kernel" [lv]="lv_kernel<10>" )
+                  [proxy_t]="proxy_mfma_buf_kernel" [lv]="lv_kernel<10>"
+                  [c4_persistent]="greedy_persistent<4, false, 9, 512, 1, true, false>" )
+declare -A EXCL=( [c4_persistent]="@none@" )
 KEYS=("$@")
 [[ ${#KEYS[@]} -gt 0 ]] || KEYS=(energy ksd_c2 proxy_gauss proxy_t lv)
 for key in "${KEYS[@]}"; do
@@ -26,6 +30,7 @@ for key in "${KEYS[@]}"; do
   f=$(find gpurun_out/pmc/${key}_FETCH_SIZE -name '*counter_collection.csv' | head -n 1)
   w=$(find gpurun_out/pmc/${key}_WRITE_SIZE -name '*counter_collection.csv' | head -n 1)
   cp "$f" gpurun_out/pmc/${key}_fetch_size.csv && cp "$w" gpurun_out/pmc/${key}_write_size.csv
-  python3 tools/summarize_pmc.py "$f" "$w" "$key" --kernel "${KERN[$key]}" --out gpurun_out/pmc/pmc_traffic_new.json || exit 1
+  python3 tools/summarize_pmc.py "$f" "$w" "$key" --kernel "${KERN[$key]}" --exclude "${EXCL[$key]:-, true, }" \
+    --source "${PMC_SOURCE:-scripts/pmc_workloads.sh}" --out gpurun_out/pmc/pmc_traffic_new.json || exit 1
 done
 echo "=== done"

@@ -64,7 +64,8 @@ def test_sharded_equals_single_process(tmp_path, world, gf):
 def _dropin_worker(rank, world, port, m, out_dir, differ):
     """The drop-in stein_thinning.thinning.thin / thin_gf called on every rank of a gloo group: rows
     sharded across the ranks (thin_across_ranks), CPU stand-in for the HIP shard backend."""
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='rccl')
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='rccl',
+                      ST_SHARD_THIN='1')
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
         from stein_thinning import distributed as sd
@@ -104,6 +105,35 @@ def test_dropin_thin_rejects_different_problems_per_rank(tmp_path):
     mp.spawn(_dropin_worker, args=(2, _free_port(), 10, str(tmp_path), True), nprocs=2, join=True)
     for r in range(2):
         assert bool(np.load(tmp_path / f'err{r}.npy')[0])
+
+
+def _optin_worker(rank, world, port, out_dir):
+    """Row sharding of the drop-in thin is opt-in: off by default under a multi-rank launch (a rank
+    may thin alone -- nothing collective runs), on with ST_SHARD_THIN=1 or set_rank_sharding(True)."""
+    os.environ.pop('ST_SHARD_THIN', None)
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from stein_thinning import thinning as st
+        got = [st._rank_sharding()]
+        os.environ['ST_SHARD_THIN'] = '1'
+        got.append(st._rank_sharding())
+        st.set_rank_sharding(False)
+        got.append(st._rank_sharding())
+        os.environ.pop('ST_SHARD_THIN')
+        st.set_rank_sharding(True)
+        got.append(st._rank_sharding())
+        st.set_rank_sharding(None)
+        got.append(st._rank_sharding())
+        np.save(os.path.join(out_dir, f'optin{rank}.npy'), np.array(got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dropin_row_sharding_is_opt_in(tmp_path):
+    mp.spawn(_optin_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    for r in range(2):
+        assert np.load(tmp_path / f'optin{r}.npy').tolist() == [False, True, False, True, False]
 
 
 def test_shard_bounds_cover_rows():

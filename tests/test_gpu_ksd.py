@@ -126,3 +126,43 @@ def test_ksd_sharded_processes(tmp_path):
     want = o.ksd(ref, 1800)
     for r in range(2):
         np.testing.assert_allclose(np.load(tmp_path / f'ks{r}.npy'), want, rtol=1e-12)
+
+
+@pytest.mark.parametrize('gf', [False, True])
+def test_colsum_per_pair_rule_independent_of_row_shards(gf):
+    """Compact setting with a few rows outside [2^-60, 2^60] (tiny gradient coordinates): every pair
+    takes the arithmetic the per-pair rule gives it (stein_math.hpp pair_value_sel) whatever tile or
+    row shard it falls in, so each shard's column sums equal, bit for bit, the sequential sums of the
+    C bit model's compact-rule pair values over that shard's rows."""
+    from stein_thinning import _native as nat
+    if nat.arithmetic() != 'compact':
+        pytest.skip('compact arithmetic not selected')
+    n, d = 900, 4
+    rng = np.random.default_rng(21)
+    x = rng.normal(size=(n, d))
+    g = -x + 0.1 * rng.normal(size=(n, d))
+    for r in (10, 300, 301, 777):
+        g[r, 1] = 1e-25          # standardised: ~1e-25 < 2^-60 -> these rows' pairs take the exact form
+    if gf:
+        with warnings.catch_warnings():
+            warnings.simplefilter('ignore')
+            dev = st._make_stein_gf_integrand(x, -0.5 * np.sum(x * x, 1), -0.45 * np.sum(x * x, 1), g,
+                                              preconditioner='med')
+    else:
+        dev = st._make_stein_integrand(x, g, preconditioner='med')
+    s, gs, w = dev.sample, dev.gradient, dev.weights
+    assert not oracle_c.compact_ok(s[[10]], gs[[10]], dev.linv_scale, dev.linv_trace)
+    be = HipKsdBackend(dev, n)
+    ii, aa = np.tril_indices(n, -1)            # column i, row a < i (row-major: a increasing per i)
+    kv = oracle_c.pairs(s, gs, None, dev.linv_scale, dev.linv_trace, ii, aa, arith='compact')
+    if gf:
+        kv = (kv * w[ii]) * w[aa]
+    for a0, a1 in [(0, n)] + [triangle_row_bounds(n, r, 3) for r in range(3)] + [(5, 301), (301, 302)]:
+        got = be.colsum(a0, a1).cpu().numpy()
+        want = np.zeros(n)
+        sel = (aa >= a0) & (aa < a1)
+        for i in range(n):
+            v = kv[sel & (ii == i)]
+            if v.size:
+                want[i] = np.cumsum(v)[-1]     # sequential, in increasing a (the kernel's order)
+        np.testing.assert_array_equal(got, want, err_msg=f'rows [{a0}, {a1})')

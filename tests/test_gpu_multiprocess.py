@@ -127,9 +127,11 @@ def test_replicated_engine_processes_share_one_gpu(tmp_path):
 
 
 def _dropin_worker(rank, world, port, out_dir):
-    """The reference's call surface, unchanged, on every rank of a 2-process group: thin / thin_gf
-    shard their rows across the ranks (thinning._greedy_search -> distributed.thin_across_ranks)."""
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device')
+    """The reference's call surface, unchanged, on every rank of a 2-process group that opted in to
+    row sharding (ST_SHARD_THIN=1): thin / thin_gf shard their rows across the ranks
+    (thinning._greedy_search -> distributed.thin_across_ranks)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device',
+                      ST_SHARD_THIN='1')
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:
@@ -272,8 +274,10 @@ def _config5_worker(rank, world, port, out_dir, m):
     """One of `world` ranks of config 5 (n = 5e5, d = 50, gradient-free) on the shared GPU through the
     drop-in thin_gf; grids capped to 256 / world blocks, so each rank's 62 500 rows exceed the wide
     persistent kernel's 256 rows per block and the launch-per-step engine with the mailbox exchange
-    kernel runs (on an 8-GPU node every rank has its own 256 CUs and the wide persistent kernel)."""
-    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device')
+    kernel runs (on an 8-GPU node every rank has its own 256 CUs and the wide persistent kernel).
+    Row sharding of the drop-in call is opted in (ST_SHARD_THIN=1)."""
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device',
+                      ST_SHARD_THIN='1')
     torch.cuda.set_device(0)
     dist.init_process_group('gloo', rank=rank, world_size=world)
     try:

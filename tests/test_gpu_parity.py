@@ -341,6 +341,36 @@ def test_compact_only_kernel_and_handoff(case):
     assert np.array_equal(gA, A, equal_nan=True)
 
 
+@pytest.mark.parametrize('case', ['in_range', 'tiny_rows_one_block'])
+def test_streamed_sums_in_lds_option(case):
+    """st_tune key 15 = 1 keeps the streamed rows' running sums in LDS (measured slower, off by
+    default): with the grid capped at 128 blocks, n = 1.1e6 leaves ~1 700 streamed rows per block;
+    the compact-only kernel (and, after a handoff, the general one) give the C model's indices and
+    running sums bit for bit either way."""
+    from stein_thinning import _native
+    n, m, d = 1_100_003, 30, 4
+    x, g = _rw_chain(n, d, seed=37)
+    s, gs = o._validate_and_standardize(x, g, True)
+    s, gs = s.copy(), gs.copy()
+    if case == 'tiny_rows_one_block':
+        s[500_000:500_010, 1] = 1e-30
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    prob = DeviceProblem(s, gs, None, l, tr)
+    cidx, cA = oracle_c.greedy_mt(s, gs, None, l, tr, m)
+    L = _native.lib()
+    assert L.st_tune(5, 128) == 0
+    try:
+        for sal in (0, 1):
+            assert L.st_tune(15, sal) == 0
+            idx, A = prob.greedy(m, return_sums=True)
+            np.testing.assert_array_equal(idx, cidx)
+            assert np.array_equal(A, cA), (sal, np.flatnonzero(A != cA)[:10])
+    finally:
+        L.st_tune(15, -1)
+        L.st_tune(5, -1)
+
+
 @pytest.mark.parametrize('d', [2, 4, 9, 50])
 def test_pair_values_bit_exact_vs_c_model(d):
     x, g = _rw_chain(700, d, seed=100 + d)

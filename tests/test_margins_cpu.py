@@ -1,0 +1,42 @@
+"""Near-tie diagnostics, CPU tier: the margin / error-band rule of
+stein_thinning.diagnostics restated over the C bit model (tests/margins_ref.py).
+
+* On an input built to have near ties (every row has a twin a few ulps away), the compact arithmetic
+  departs from the NumPy path's selection, and the step where it first departs is flagged; the exact
+  arithmetic reproduces NumPy's indices there.
+* On the reference's golden problem (F1, Gradient_free_Stein_thinning.ipynb cell 8) no step is
+  flagged: its margins are ~1e12 ulps against bands of a few thousand."""
+import numpy as np
+
+from oracle import models
+from oracle import stein_numpy as o
+from tests import margins_ref as mr
+
+
+def _std(x, g):
+    s, gs = o._validate_and_standardize(x, g, True)
+    linv = o.make_precon(s, 'id')
+    return s, gs, linv[0, 0], np.trace(linv)
+
+
+def test_near_tie_divergence_is_flagged():
+    X, G = mr.near_tie_twins(0)
+    s, gs, l, tr = _std(X, G)
+    want = o.thin(X, G, 30)
+    exact = mr.margins(s, gs, None, l, tr, 30, 'exact')
+    np.testing.assert_array_equal(exact['indices'], want)
+    comp = mr.margins(s, gs, None, l, tr, 30, 'compact')
+    bad = np.flatnonzero(comp['indices'] != want)
+    assert bad.size, 'the construction should make the compact arithmetic depart from NumPy'
+    assert comp['flagged'][:bad[0] + 1].any(), 'the departure must be inside a flagged step'
+    assert comp['flagged'][bad[0]]
+    assert comp['margin_ulps'][bad[0]] < 100 < 1e6 < comp['margin_ulps'][0]
+
+
+def test_golden_problem_has_no_flags():
+    sample, gradient, _, _, _ = models.bivariate_reference_sample(1000)
+    s, gs, l, tr = _std(sample, gradient)
+    for arith in ('compact', 'exact'):
+        r = mr.margins(s, gs, None, l, tr, 20, arith)
+        assert not r['flagged'].any()
+        assert r['margin_ulps'].min() > 1e9 and r['band_ulps'].max() < 1e5

@@ -27,6 +27,7 @@ def main():
     ap.add_argument('--kernel', default='greedy_step_ct')
     ap.add_argument('--exclude', default=', true, ')   # template arg DIAG=true -> diagonal launch
     ap.add_argument('--out', default='profiles/pmc_traffic.json')
+    ap.add_argument('--source', default='', help='which pass this was (round, script, commit): kept in the record')
     args = ap.parse_args()
     f, w = load(args.fetch_csv), load(args.write_csv)
 
@@ -44,6 +45,8 @@ def main():
            'read_bytes_per_launch': 2 * fetch_kib * 1024, 'write_bytes_per_launch': write_kib * 1024,
            'hbm_bytes_per_launch': (2 * fetch_kib + write_kib) * 1024,
            'correction': 'FETCH_SIZE x2 (gfx950 half-count of wide coalesced reads); KiB -> bytes'}
+    if args.source:
+        rec['source'] = args.source
     out = json.load(open(args.out)) if os.path.exists(args.out) else {}
     out[args.config] = rec
     json.dump(out, open(args.out, 'w'), indent=1)
