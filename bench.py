@@ -127,6 +127,10 @@ CONFIGS = {
     'c4': dict(desc='LV-surrogate pooled d=4 n=2e6 Langevin IMQ med m=1000', n=2_000_000, m=1000, gf=False, seed=12345),
     'c5': dict(desc='Gaussian AR(1) d=50 n=5e5 gradient-free IMQ med m=500', n=500_000, m=500, gf=True, seed=12349,
                d50=True),
+    # one rank's share of an 8-GPU config-4 run (2.5e5 rows, m = 1000): the per-GPU load of that run,
+    # for the same-device rehearsals of the rank exchange (DESIGN.md section 5 cost model)
+    'c4r8': dict(desc='LV-surrogate d=4 n=2.5e5 (one rank of 8 of config 4) Langevin IMQ med m=1000', n=250_000,
+                 m=1000, gf=False, seed=12345),
     # the reference's LV call (not a BASELINE config): one chain of 5e5, m = 10 000, 'med'
     'lv': dict(desc="LV call shape: thin(np.exp(s), grads, 10_000, 'med') on one RW-MH chain n=5e5 "
                     "(Stein_thinning.ipynb:204)", n=500_000, m=10_000, gf=False, seed=12350, lv_shape='exp'),
@@ -572,7 +576,7 @@ def main():
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic (seeded RW-MH LV-surrogate chains; see bench.py docstring)',
-            'config': {'workload': (f"config {args.config[1]}: {cfg['desc']}" if args.config[0] == 'c' else cfg['desc']),
+            'config': {'workload': (f"config {args.config[1]}: {cfg['desc']}" if args.config in ('c2', 'c3', 'c4', 'c5') else cfg['desc']),
                        'n': n, 'd': d, 'm': m,
                        'preconditioner': 'med', 'kernel': 'gradient-free' if integrand.weights is not None else 'langevin',
                        'parallelism': (f'rows-sharded x{world}, per-step exchange: {runner.mode}'

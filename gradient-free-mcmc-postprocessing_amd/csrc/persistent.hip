@@ -193,6 +193,7 @@ struct PersistArgs {
     int64_t rows_per_block;
     int RL;               // LDS-resident rows per block
     int stream_a_lds;     // 512-thread kernels: the streamed rows' running sums are kept in LDS
+    int poll_delay;       // s_memrealtime ticks added before aligning a step's first poll (st_tune key 16)
     uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
     int rec_stride;               // record pitch in granules (2 = packed; wider spreads the polled
                                   // records over more memory channels)
@@ -346,6 +347,10 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 #ifndef ST_POLL_SYNC_FIRST
 #define ST_POLL_SYNC_FIRST 1
 #endif
+#ifndef ST_FINAL_ROWLOAD
+#define ST_FINAL_ROWLOAD 0
+#endif
+
 
 // wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
 // (np.argmin order).  Lane L owns records L, L+64, L+128, L+192 and re-polls only those it has not
@@ -469,7 +474,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             u32x4 qs[MAXG / 64];
 #if ST_POLL_SYNC > 0
             if (ST_POLL_SYNC_FIRST || it > 0) {   // polls on a chip-wide grid of ST_POLL_SYNC ticks
-                const uint64_t now = __builtin_amdgcn_s_memrealtime();
+                const uint64_t now = __builtin_amdgcn_s_memrealtime() + (it == 0 ? (uint64_t)a.poll_delay : 0);
                 const uint64_t slot = (now + ST_POLL_SYNC - 1) / ST_POLL_SYNC * ST_POLL_SYNC;
                 while (__builtin_amdgcn_s_memrealtime() < slot) __builtin_amdgcn_s_sleep(1);
             }
@@ -508,7 +513,18 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                 if (si != spec_prev) { spec_prev = si; spec_settle = it + 1; }
             }
 #endif
-            if (__all(seen == need)) break;
+            if (__all(seen == need)) {
+#if ST_FINAL_ROWLOAD
+                // a sweep that completed on its FIRST poll has no speculative row in flight: every
+                // lane starts loading its own best's row now, so the winner's arrives while the wave
+                // minloc runs instead of after it (later polls keep the rows loaded between polls)
+                if (it == 0 && bi != 0xFFFFFFFFu) {
+                    load_row((int64_t)bi);
+                    row_of = (int64_t)bi;
+                }
+#endif
+                break;
+            }
             if (!between()) break;
             __builtin_amdgcn_s_sleep(1);
         }
@@ -1115,6 +1131,14 @@ static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register
 // LDS from ~120 LDS rows, which then stream (~1.1 ns instead of ~0.36 ns per row-step), and the A
 // load / store it saves was not on the critical path (L2-resident, stores fire-and-forget).
 static int g_persist_sal = 0;
+// st_tune key 16: ticks (10 ns) added to a step's first poll time before it is aligned to the poll
+// grid: -1 auto = 10 for the one-device compact-only kernel, 0 otherwise.  A block whose first poll
+// would fall just before the last records land takes the next grid slot instead of an early,
+// incomplete poll.  Round 4, same box, two sweeps (profiles/r04_first_poll_delay.log): n = 2e6
+// (compact-only kernel) 7.10 / 7.21 (0) -> 6.80 / 6.88 us per step (10), 5: 6.82 / 6.91, 15: 6.83 /
+// 6.86, 20 and 25 slower; n = 1e6 and 4e5 (general 512-thread kernel) and 2e5 / 2.5e5 (256-thread
+// kernels): every delay slower or equal.
+static int g_persist_delay = -1;
 // automatic register rows of the compact-only kernel: 9 (28 B of scratch at d = 4) unless more than
 // kCmpStreamRows rows per block would still be streamed, then 10 (108 B of scratch; the streamed
 // rows then no longer stay in the XCD's L2).  Same-box, d = 4, m = 1000 (profiles/r03_compact_only_rt.log):
@@ -1159,6 +1183,11 @@ int persistent_tune(int key, int value) {
     if (key == 12) {
         if (value != -1 && value != 0 && (value < 8 || value > 10)) return -1;
         g_persist_cmp = value;
+        return 0;
+    }
+    if (key == 16) {
+        if (value < -1 || value > 450) return -1;
+        g_persist_delay = value;
         return 0;
     }
     if (key == 15) {
@@ -1348,6 +1377,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.rows_per_block = R;
     a.RL = (int)RL;
     a.stream_a_lds = sal;
+    a.poll_delay = g_persist_delay >= 0 ? g_persist_delay : 0;
     a.rec_stride = pitch;
     a.nrep = nrep;
     a.rep_stride = persistent_rep_stride(G, pitch, nrep);
@@ -1377,6 +1407,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         lds_rows(512, rt_c, RLc, lds_c, salc);
         ac.RL = (int)RLc;
         ac.stream_a_lds = salc;
+        ac.poll_delay = g_persist_delay >= 0 ? g_persist_delay : 10;
         use_cmp = offsets_ok(512, rt_c, RLc) &&
                   launch_cmp(ac, d, gf, rt_c, G, lds_c, s, true) == hipSuccess;   // residency check only
     }

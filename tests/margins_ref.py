@@ -7,19 +7,21 @@ from stein_thinning.diagnostics import BAND_ULPS_PER_TERM
 from tests import oracle_c
 
 
-def near_tie_twins(seed: int = 0, n: int = 400, nudge: int = 4):
-    """Bivariate Gaussian (Gradient_free_Stein_thinning.ipynb's target) plus a twin of every row with
-    x[:, 0] moved by `nudge` ulps: every selected row has a runner-up a few ulps of its running sum
-    away, so the selection rests on pair values' last bits (seed 0: the exact arithmetic reproduces
-    NumPy's 30 indices, the compact one departs from them)."""
+def near_tie_twins(seed: int = 0, n: int = 400, nudge: int = 4, steps=(8, 9, 10, 11, 12)):
+    """Bivariate Gaussian (Gradient_free_Stein_thinning.ipynb's target, n rows) plus a twin of each row
+    the NumPy path selects at `steps`, with x[:, 0] moved by `nudge` ulps (same score): at those steps
+    the winner has a runner-up a few ulps of its running sum away and the selection rests on the pair
+    values' last bits.  Returns (x, g, steps)."""
+    from oracle import stein_numpy as o
     rng = np.random.default_rng(seed)
     cov = np.array([[1, .8], [.8, 1]])
     x = rng.multivariate_normal([0, 0], cov, size=n)
     g = -np.linalg.solve(cov, x.T).T
-    xt = x.copy()
+    pick = o.thin(x, g, max(steps) + 1)[list(steps)]
+    xt = x[pick].copy()
     for _ in range(nudge):
         xt[:, 0] = np.nextafter(xt[:, 0], np.inf)
-    return np.vstack([x, xt]), np.vstack([g, g])
+    return np.vstack([x, xt]), np.vstack([g, g[pick]]), np.array(steps)
 
 
 def _scale(s, gs, j, l, tr):
@@ -48,12 +50,17 @@ def margins(s, gs, w, l, tr, m, arith):
             band = band + 2.0 * c * np.spacing(np.abs(sc)) + np.spacing(np.abs(A))
         b = int(np.argmin(A))
         best = A[b]
-        rest = np.where(A == best, np.inf, A)
+        eq = A == best
+        rest = np.where(eq, np.inf, A)
         r = int(np.argmin(rest))
         ub = np.spacing(abs(best))
         gap = rest[r] - best
+        # rows tied with the winner that are not exact duplicates of it tie only by accident
+        same = np.all(s[eq] == s[b], axis=1) & np.all(gs[eq] == gs[b], axis=1)
+        if w is not None:
+            same &= w[eq] == w[b]
         out['indices'].append(b)
         out['margin_ulps'].append(gap / ub)
         out['band_ulps'].append((band[b] + band[r]) / ub)
-        out['flagged'].append(bool(gap <= band[b] + band[r]))
+        out['flagged'].append(bool(gap <= band[b] + band[r]) or not bool(same.all()))
     return {k: np.array(v) for k, v in out.items()}

@@ -23,7 +23,7 @@ from stein_thinning import thinning as st  # noqa: E402
 
 @pytest.mark.parametrize('arith', ['compact', 'exact'])
 def test_margins_match_bit_model_and_flag_the_near_tie(arith):
-    X, G = mr.near_tie_twins(0)
+    X, G, steps = mr.near_tie_twins(0)
     want = o.thin(X, G, 30)
     stein_thinning.set_arithmetic(arith)
     try:
@@ -38,6 +38,7 @@ def test_margins_match_bit_model_and_flag_the_near_tie(arith):
     np.testing.assert_array_equal(gm.margin_ulps, ref['margin_ulps'])
     np.testing.assert_allclose(gm.band_ulps, ref['band_ulps'], rtol=1e-6)
     np.testing.assert_array_equal(gm.flagged, ref['flagged'])
+    np.testing.assert_array_equal(gm.flagged_steps(), steps)
     if arith == 'exact':
         np.testing.assert_array_equal(idx, want)
     else:

@@ -20,17 +20,25 @@ def _std(x, g):
 
 
 def test_near_tie_divergence_is_flagged():
-    X, G = mr.near_tie_twins(0)
-    s, gs, l, tr = _std(X, G)
-    want = o.thin(X, G, 30)
-    exact = mr.margins(s, gs, None, l, tr, 30, 'exact')
-    np.testing.assert_array_equal(exact['indices'], want)
-    comp = mr.margins(s, gs, None, l, tr, 30, 'compact')
-    bad = np.flatnonzero(comp['indices'] != want)
-    assert bad.size, 'the construction should make the compact arithmetic depart from NumPy'
-    assert comp['flagged'][:bad[0] + 1].any(), 'the departure must be inside a flagged step'
-    assert comp['flagged'][bad[0]]
-    assert comp['margin_ulps'][bad[0]] < 100 < 1e6 < comp['margin_ulps'][0]
+    """Twins (a few ulps apart) of the rows NumPy selects at steps 8-12: exactly those steps are
+    flagged in both arithmetics; the exact arithmetic reproduces NumPy's 30 indices on every seed,
+    the compact one departs from them at a flagged step (on 9 of these 10 seeds)."""
+    departed = 0
+    for seed in range(10):
+        X, G, steps = mr.near_tie_twins(seed)
+        s, gs, l, tr = _std(X, G)
+        want = o.thin(X, G, 30)
+        exact = mr.margins(s, gs, None, l, tr, 30, 'exact')
+        np.testing.assert_array_equal(exact['indices'], want)
+        np.testing.assert_array_equal(np.flatnonzero(exact['flagged']), steps)
+        comp = mr.margins(s, gs, None, l, tr, 30, 'compact')
+        np.testing.assert_array_equal(np.flatnonzero(comp['flagged']), steps)
+        bad = np.flatnonzero(comp['indices'] != want)
+        if bad.size:
+            departed += 1
+            assert comp['flagged'][bad[0]], seed
+        assert comp['margin_ulps'][steps].min() < 1e3 and comp['margin_ulps'][:8].min() > 1e9
+    assert departed >= 5
 
 
 def test_golden_problem_has_no_flags():
