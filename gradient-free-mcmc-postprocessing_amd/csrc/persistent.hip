@@ -248,10 +248,15 @@ constexpr int kRecGranules = 2;
 // more memory channels than 16-B packing (-0.3 us per step, profiles/r01_sweep_pitch.log)
 constexpr int kDefaultRecPitch = 256;
 // replicas of the record array (st_tune key 10): every block stores its record into each replica
-// (16-B sc1 stores by 16 lanes) and block b sweeps replica b % 16, densely packed: 16 readers per
-// line instead of 256, 32 lines per poll instead of 256.  Config 4: 11.6 -> 11.1 ms per thin;
-// n = 2.5e5 per device (one rank of 8): 4.80 -> 4.47 us per step (profiles/r02_record_replicas.log)
-constexpr int kDefaultRecReplicas = 16;
+// (16-B sc1 stores by 8 lanes) and block b sweeps replica b % 8, densely packed: 32 readers per
+// line instead of 256, 32 lines per poll instead of 256.  Round 2 (16 replicas): config 4 11.6 ->
+// 11.1 ms per thin; n = 2.5e5 per device (one rank of 8): 4.80 -> 4.47 us per step
+// (profiles/r02_record_replicas.log).  Round 4, the round-4 kernel, same box, two sweeps
+// (profiles/r04_replicas_nt_sweep.log): 8 replicas against 16 -- config 2 3.32 vs 3.41 / 3.46 us per
+// step, 2.5e5 rows 3.31 / 3.32 vs 3.34, config 4 6.82 / 6.84 vs 6.89 (4 replicas within 0.01 of 8, 32
+// slower); the flat-sweep probe without pair arithmetic agrees (1.80 vs 2.15 us per step,
+// profiles/r04_flat_sweep_probe.log)
+constexpr int kDefaultRecReplicas = 8;
 constexpr int64_t kNt512MinRows = 1280;
 
 __device__ __forceinline__ uint64_t step_tag(int64_t t) { return (uint64_t)((t + 1) & 0xFF) << 56; }
@@ -347,9 +352,7 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 #ifndef ST_POLL_SYNC_FIRST
 #define ST_POLL_SYNC_FIRST 1
 #endif
-#ifndef ST_FINAL_ROWLOAD
-#define ST_FINAL_ROWLOAD 0
-#endif
+
 
 
 // wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
@@ -513,18 +516,9 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                 if (si != spec_prev) { spec_prev = si; spec_settle = it + 1; }
             }
 #endif
-            if (__all(seen == need)) {
-#if ST_FINAL_ROWLOAD
-                // a sweep that completed on its FIRST poll has no speculative row in flight: every
-                // lane starts loading its own best's row now, so the winner's arrives while the wave
-                // minloc runs instead of after it (later polls keep the rows loaded between polls)
-                if (it == 0 && bi != 0xFFFFFFFFu) {
-                    load_row((int64_t)bi);
-                    row_of = (int64_t)bi;
-                }
-#endif
-                break;
-            }
+            // (loading every lane's best row here when the first poll completes the sweep, before the
+            // wave minloc, was measured +0.9 us per step: profiles/r04_single_poll_rowload_rejected.log)
+            if (__all(seen == need)) break;
             if (!between()) break;
             __builtin_amdgcn_s_sleep(1);
         }
@@ -1113,9 +1107,10 @@ int64_t persistent_ws_bytes(int d, int G, int rec_stride, int nrep) {
 }
 
 // workspace the persistent launcher can use at most: two record regions (compact-only kernel and
-// the general kernel gated behind it) at the widest grid, default replicas and packed records
+// the general kernel gated behind it) at the widest grid, the most replicas st_tune key 10 allows and
+// packed records
 int64_t persistent_ws_max_bytes() {
-    return kWsControlBytes + 2 * persistent_region_bytes(kMaxGrid, kRecGranules, kDefaultRecReplicas);
+    return kWsControlBytes + 2 * persistent_region_bytes(kMaxGrid, kRecGranules, 32);
 }
 
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
