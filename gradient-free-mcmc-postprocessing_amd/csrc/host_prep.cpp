@@ -19,6 +19,8 @@
 #include <thread>
 #include <vector>
 
+#include <emmintrin.h>
+
 #include "../../include/stein_thinning_hip.h"
 
 namespace {
@@ -60,6 +62,60 @@ int hardware_threads() {
     return h == 0 ? 1 : (int)std::min(h, 16u);
 }
 
+// d = 2 .. 8: both column passes over x by ONE thread, every column's sequential sum in registers
+// (one stream of the array instead of one per column thread, each of which had to fetch every cache
+// line), with x's NaN / inf flags taken in the first pass; g is scanned by the other threads meanwhile.
+template <int D>
+void column_stats(const double* x, int64_t n, double* loc, double* scl, int& nan, int& inf) {
+    double acc[D];
+    int fn = 0, fi = 0;
+#pragma unroll
+    for (int j = 0; j < D; ++j) {
+        acc[j] = x[j];
+        fn |= (int)(x[j] != x[j]);
+        fi |= (int)(fabs(x[j]) == INFINITY);
+    }
+    for (int64_t i = 1; i < n; ++i) {
+        const double* row = x + i * D;
+        __builtin_prefetch(row + 64 * D);
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            acc[j] += row[j];
+            fn |= (int)(row[j] != row[j]);
+            fi |= (int)(fabs(row[j]) == INFINITY);
+        }
+    }
+    nan = fn;
+    inf = fi;
+    if (fn | fi) return;
+    const double dn = (double)n;
+    double l[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) { l[j] = acc[j] / dn; acc[j] = fabs(x[j] - l[j]); }
+    for (int64_t i = 1; i < n; ++i) {
+        const double* row = x + i * D;
+        __builtin_prefetch(row + 64 * D);
+#pragma unroll
+        for (int j = 0; j < D; ++j) acc[j] += fabs(row[j] - l[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) { loc[j] = l[j]; scl[j] = acc[j] / dn; }
+}
+
+using StatsFn = void (*)(const double*, int64_t, double*, double*, int&, int&);
+StatsFn stats_for(int d) {
+    switch (d) {
+        case 2: return column_stats<2>;
+        case 3: return column_stats<3>;
+        case 4: return column_stats<4>;
+        case 5: return column_stats<5>;
+        case 6: return column_stats<6>;
+        case 7: return column_stats<7>;
+        case 8: return column_stats<8>;
+        default: return nullptr;
+    }
+}
+
 }  // namespace
 
 extern "C" int st_standardize_host(const double* sample, const double* gradient, int64_t n,
@@ -79,10 +135,34 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
         for (int t = 0; t < T; ++t) th.emplace_back([&fn, t, T] { fn(t, T); });
         for (auto& x : th) x.join();
     };
+    std::vector<double> loc(d, 0.0), scl(d, 0.0);
+    const double dn = (double)n;
+    StatsFn fast = standardize && n >= 65536 ? stats_for(d) : nullptr;
+    if (fast) {
+        // thread 0: x's flags, column sums and absolute deviations; the others: g's flags
+        const int tg = std::max(1, hw - 1);
+        std::vector<int> nanf(tg + 1, 0), inff(tg + 1, 0);
+        parallel(tg + 1, [&](int t, int) {
+            if (t == 0) {
+                fast(sample, n, loc.data(), scl.data(), nanf[0], inff[0]);
+                return;
+            }
+            bool nan = false, inf = false;
+            for (int64_t e = total * (t - 1) / tg; e < total * t / tg; ++e) {
+                const double gv = gradient[e];
+                nan |= gv != gv;
+                inf |= fabs(gv) == INFINITY;
+            }
+            nanf[t] = nan;
+            inff[t] = inf;
+        });
+        for (int t = 0; t <= tg; ++t) if (nanf[t]) { *status = 1; return ST_OK; }
+        for (int t = 0; t <= tg; ++t) if (inff[t]) { *status = 2; return ST_OK; }
+    }
     // pass 1: NaN / inf flags (NaN reported first, as the NumPy checks run in that order)
     const int tn = (int)std::max<int64_t>(1, std::min<int64_t>(hw, total / (1 << 18)));
     std::vector<int> nanf(tn, 0), inff(tn, 0);
-    parallel(tn, [&](int t, int T) {
+    if (!fast) parallel(tn, [&](int t, int T) {
         bool nan = false, inf = false;
         for (int64_t e = total * t / T; e < total * (t + 1) / T; ++e) {
             const double xv = sample[e], gv = gradient[e];
@@ -99,9 +179,9 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
         if (gradient_out != gradient) memcpy(gradient_out, gradient, (size_t)total * 8);
         return ST_OK;
     }
-    std::vector<double> loc(d, 0.0), scl(d, 0.0);
-    const double dn = (double)n;
-    if (d == 1) {
+    if (fast) {
+        // loc, scl done above
+    } else if (d == 1) {
         loc[0] = numpy_column_sum(sample, n) / dn;
         std::vector<double> dev((size_t)n);
         for (int64_t i = 0; i < n; ++i) dev[i] = fabs(sample[i] - loc[0]);
@@ -130,8 +210,41 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
         if (scl[j] == 0.0) { *status = 3; return ST_OK; }
     if (loc_out) memcpy(loc_out, loc.data(), (size_t)d * 8);
     if (scl_out) memcpy(scl_out, scl.data(), (size_t)d * 8);
-    // pass 3: x / scl, g * scl -- elementwise, row blocks in parallel
+    // pass 3: x / scl, g * scl -- elementwise, row blocks in parallel.  Large 16-B-aligned outputs
+    // (the page-locked upload buffers) are written with non-temporal stores, two elements per
+    // instruction (IEEE division / multiplication either way: the same bits): no read-for-ownership
+    // of lines that are only written, and nothing the upload reads back evicted from the caches
     const int nt = (int)std::max<int64_t>(1, std::min<int64_t>(hw, n / 65536));
+    const bool nt_ok = n >= 65536 && d <= 64 && ((uintptr_t)sample_out % 16 == 0) &&
+                       ((uintptr_t)gradient_out % 16 == 0) && ((uintptr_t)sample % 8 == 0) &&
+                       ((uintptr_t)gradient % 8 == 0);
+    if (nt_ok) {
+        std::vector<double> rep(2 * (size_t)d + 2);   // scl repeated: rep[k .. k+1] = scl[k % d], scl[(k+1) % d]
+        for (size_t k = 0; k < rep.size(); ++k) rep[k] = scl[k % d];
+        parallel(nt, [&](int t, int T) {
+            int64_t e0 = total * t / T;
+            const int64_t e1 = total * (t + 1) / T;
+            e0 += e0 & 1;                                // even start: 16-B aligned output
+            auto scalar = [&](int64_t e) {
+                sample_out[e] = sample[e] / scl[e % d];
+                gradient_out[e] = gradient[e] * scl[e % d];
+            };
+            int64_t e = e0;
+            int k = (int)(e % d);
+            for (; e + 1 < e1; e += 2) {
+                const __m128d sv = _mm_loadu_pd(rep.data() + k);
+                _mm_stream_pd(sample_out + e, _mm_div_pd(_mm_loadu_pd(sample + e), sv));
+                _mm_stream_pd(gradient_out + e, _mm_mul_pd(_mm_loadu_pd(gradient + e), sv));
+                k += 2;
+                while (k >= d) k -= d;   // (d = 1: twice)
+            }
+            for (; e < e1; ++e) scalar(e);
+            // the element this thread's range skipped to start even belongs to the previous thread
+            if (t > 0 && ((total * t / T) & 1)) scalar(total * t / T);
+            _mm_sfence();
+        });
+        return ST_OK;
+    }
     parallel(nt, [&](int t, int T) {
         for (int64_t i = n * t / T; i < n * (t + 1) / T; ++i)
             for (int j = 0; j < d; ++j) {

@@ -58,7 +58,11 @@ class DeviceProblem:
             self.w = w
 
     def _soa(self, torch, rowmajor: np.ndarray):
-        rm = torch.from_numpy(rowmajor).to(self.device, non_blocking=False)
+        # page-locked host arrays (thinning._host_buffer) go up asynchronously on the current stream:
+        # the caller keeps them alive (SteinIntegrand holds them) and the layout kernel is queued
+        # behind the copy, so host work after this call (the 'med' preconditioner) overlaps the DMA
+        src = torch.from_numpy(rowmajor)
+        rm = src.to(self.device, non_blocking=bool(src.is_pinned()))
         soa = torch.zeros((self.d, self.ld), dtype=torch.float64, device=self.device)
         nat.check(nat.lib().st_layout_soa(nat.ptr(rm), self.n, self.d, self.ld, nat.ptr(soa),
                                           nat.stream_handle()), 'st_layout_soa')

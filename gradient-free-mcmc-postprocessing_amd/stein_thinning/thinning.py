@@ -214,10 +214,32 @@ class SteinIntegrand:
         return out.reshape(b1.shape)
 
 
+def _early_upload(sample: np.ndarray, gradient: np.ndarray, weights: Optional[np.ndarray]):
+    """Start the device copy of standardised, page-locked host arrays before the preconditioner is
+    known (its 'med' heuristic is host work: the H2D DMA and the SoA layout run meanwhile); None when
+    the arrays are not page-locked (no HIP device) -- the integrand then uploads on first use."""
+    try:
+        import torch
+        if not (torch.cuda.is_available() and torch.from_numpy(sample).is_pinned()):
+            return None
+    except Exception:   # noqa: BLE001 -- an optimisation only
+        return None
+    from .device import DeviceProblem
+    return DeviceProblem(sample, gradient, weights, 0.0, 0.0)   # l, tr filled in with the preconditioner
+
+
+def _attach(integrand: SteinIntegrand, prob) -> SteinIntegrand:
+    if prob is not None:
+        prob.l, prob.tr = float(integrand.linv_scale), float(integrand.linv_trace)
+        integrand._problem = prob
+    return integrand
+
+
 def _make_stein_integrand(sample, gradient, standardize: bool = True, preconditioner='id') -> SteinIntegrand:
     sample, gradient = _validate_and_standardize(sample, gradient, standardize)
+    prob = _early_upload(sample, gradient, None) if preconditioner == 'med' else None
     linv = make_precon(sample, preconditioner)
-    return SteinIntegrand(sample, gradient, linv)
+    return _attach(SteinIntegrand(sample, gradient, linv), prob)
 
 
 def _make_stein_gf_integrand(sample, log_p, log_q, gradient_q, standardize: bool = True,
@@ -231,8 +253,9 @@ def _make_stein_gf_integrand(sample, log_p, log_q, gradient_q, standardize: bool
     if np.isnan(log_p).any() or np.isnan(log_q).any():
         raise ValueError('log_p or log_q contains NaNs.')
     weights = np.exp(_log_weights(log_p, log_q, range_cap))
+    prob = _early_upload(sample, gradient_q, weights) if preconditioner == 'med' else None
     linv = make_precon(sample, preconditioner)
-    return SteinIntegrand(sample, gradient_q, linv, weights)
+    return _attach(SteinIntegrand(sample, gradient_q, linv, weights), prob)
 
 
 def _greedy_search_protocol(n_points: int, integrand: Callable) -> np.ndarray:
