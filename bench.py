@@ -339,6 +339,8 @@ def main():
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
     ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
+    ap.add_argument('--lv-global-obs', type=int, default=0,
+                    help='lv workload: 1 = phase B reads the observations from global memory (st_tune key 17)')
     ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
     ap.add_argument('--energy-variant', type=int, default=0, help='energy kernel (st_tune key 13; 0 = auto)')
     ap.add_argument('--energy-units', type=int, default=-1,
@@ -971,6 +973,7 @@ def main_lv(args):
     status = torch.zeros(m, dtype=torch.int32, device=dev)
     L = nat.lib()
     two_phase = args.lv_mode == 0
+    nat.check(L.st_tune(17, args.lv_global_obs), 'st_tune')
     wb = int(L.st_lv_grad_workspace_bytes(m, t.size))
     work = torch.empty((wb + 7) // 8, dtype=torch.float64, device=dev) if two_phase else None
 
@@ -1018,7 +1021,8 @@ def main_lv(args):
             'roofline': ({'bound': 'valu', 'achieved': round(lv_flops / kern_s / 1e12, 2), 'peak': FP64_VALU_PEAK_TFS,
                           'unit': 'TFLOP/s', 'frac': round(lv_flops / kern_s / 1e12 / FP64_VALU_PEAK_TFS, 4),
                           'traffic': pmc_traffic('lv2') if world == 1 else None,
-                          'kernel': 'lv_kernel<10,record> + lv_dense_kernel (+ overflow pass)',
+                          'kernel': 'lv_kernel<10,record> + lv_dense_kernel<' +
+                                    ('4,global-obs' if args.lv_global_obs == 1 else '8,lds-obs') + '> (+ overflow pass)',
                           'kernel_avg_us': round(kern_s * 1e6, 1), 'flop_per_observation': LV_FLOP_PER_OBS,
                           'note': 'priced on the dense-output work only (n x t_n observation points x '
                                   f'{LV_FLOP_PER_OBS} flop: the quartic for 10 states, residual, C^-1 and the '

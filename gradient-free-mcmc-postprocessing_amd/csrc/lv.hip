@@ -346,10 +346,25 @@ __device__ __forceinline__ int wave_sum_int(int v) {
 // sums.  The per-point sum is thus reassociated (pieces, then a tree) against the reference's
 // sequential np.sum -- within the same 1e-8 tolerance as the BLAS-ordered stages
 // (tests/test_gpu_lv.py).
-__global__ __launch_bounds__(256) void lv_dense_kernel(LvArgs a) {
-    const int64_t i = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+// LDS: the observation times and data (3 t_n doubles, shared by every parameter point) are staged in
+// LDS once per block of WPB points and read from there.  Round 4, PMC (profiles/r04_lv_stall.json):
+// with each lane of a wave at a different observation index, every t_eval / y_obs load touched 64
+// cache lines and the texture address unit was busy ~80 % of the kernel while the VALU issued on
+// ~60 % of SIMD cycles.
+template <int WPB, bool LDS>
+__global__ __launch_bounds__(64 * WPB) void lv_dense_kernel(LvArgs a) {
+    const int64_t i = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
-    __shared__ int pstart_sh[4][65];
+    __shared__ int pstart_sh[WPB][65];
+    extern __shared__ double obs_sh[];      // LDS: t[t_n], y0[t_n], y1[t_n]
+    if constexpr (LDS) {
+        for (int e = threadIdx.x; e < a.t_n; e += 64 * WPB) {
+            obs_sh[e] = a.t_eval[e];
+            obs_sh[a.t_n + e] = a.y_obs[2 * e];
+            obs_sh[2 * a.t_n + e] = a.y_obs[2 * e + 1];
+        }
+        __syncthreads();
+    }
     if (i >= a.n) return;                   // (wave-uniform: the whole wave leaves)
     if (a.status[i] != 0) return;          // NaN already written, or the overflow kernel's point
     const int ns = a.nsteps[i];            // <= step_cap <= 64
@@ -417,9 +432,15 @@ __global__ __launch_bounds__(256) void lv_dense_kernel(LvArgs a) {
         const double c0 = a.cinv[0], c1 = a.cinv[1], c2 = a.cinv[2], c3 = a.cinv[3];
         auto obs = [&](int k, double& tk, double& o0, double& o1) {
             const int kc = k < ke ? k : ke - 1;    // past the piece: a harmless reload, unused
-            tk = a.t_eval[kc];
-            o0 = a.y_obs[2 * kc];
-            o1 = a.y_obs[2 * kc + 1];
+            if constexpr (LDS) {
+                tk = obs_sh[kc];
+                o0 = obs_sh[a.t_n + kc];
+                o1 = obs_sh[2 * a.t_n + kc];
+            } else {
+                tk = a.t_eval[kc];
+                o0 = a.y_obs[2 * kc];
+                o1 = a.y_obs[2 * kc + 1];
+            }
         };
         auto point = [&](double tk, double o0, double o1) {
             const double x = (tk - t_old) * inv_hd;
@@ -465,6 +486,16 @@ __global__ __launch_bounds__(256) void lv_dense_kernel(LvArgs a) {
 
 }  // namespace
 
+// st_tune key 17: phase B variant -- 0 / -1 auto (observations in LDS, 8 points per block: 1.31-1.32 ms
+// for 113 143 points against 1.43 with 12 per block), 1 = the observations read from global memory
+// (the round-3 kernel, 1.59-1.61 ms; profiles/r04_lv_obs_lds_ab.log)
+static int g_lv_global_obs = 0;
+int lv_tune(int value) {
+    if (value < -1 || value > 1) return -1;
+    g_lv_global_obs = value < 0 ? 0 : value;
+    return 0;
+}
+
 int64_t lv_grad_workspace_bytes(int64_t n, int step_cap) {
     return n * ((int64_t)step_cap * kLvStepRec * 8 + 8);
 }
@@ -477,7 +508,12 @@ hipError_t launch_lv(const LvArgs& a, bool gradient, hipStream_t s) {
         lv_kernel<10, true><<<blocks, kLvThreads, 0, s>>>(a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        lv_dense_kernel<<<(unsigned)((a.n + 3) / 4), 256, 0, s>>>(a);
+        // observations in LDS when they fit the default 64 KB dynamic allocation (t_n <= 2730)
+        const size_t obs_bytes = (size_t)a.t_n * 3 * sizeof(double);
+        if (obs_bytes <= 65536 && g_lv_global_obs != 1)
+            lv_dense_kernel<8, true><<<(unsigned)((a.n + 7) / 8), 512, obs_bytes, s>>>(a);
+        else
+            lv_dense_kernel<4, false><<<(unsigned)((a.n + 3) / 4), 256, 0, s>>>(a);
         if ((e = hipGetLastError()) != hipSuccess) return e;
         lv_kernel<10, false, true><<<blocks, kLvThreads, 0, s>>>(a);
         return hipGetLastError();

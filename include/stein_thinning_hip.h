@@ -84,7 +84,9 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * ticks of the 100 MHz s_memrealtime clock added to a step's first winner poll before it is aligned
  * to the chip-wide poll grid (0 .. 450; -1 = automatic = 10 for the one-device compact-only kernel,
  * 0 otherwise;
- * timing only, same results).
+ * timing only, same results), key 17 = LV gradient phase B: 1 reads the observation times / data
+ * from global memory as round 3 did (0 / -1 = automatic: staged in LDS when 3 t_n doubles fit
+ * 64 KB; same results).
  */
 int st_tune(int32_t key, int32_t value);
 
