@@ -56,13 +56,28 @@ class DeviceProblem:
             w = torch.zeros(self.ld, dtype=torch.float64, device=self.device)
             w[:self.n] = torch.from_numpy(np.ascontiguousarray(weights, dtype=np.float64)).to(self.device)
             self.w = w
+        # asynchronous uploads (page-locked sources): an event after the layout kernels, so the owner
+        # can make sure they finished before the arrays are used on another stream (wait_upload)
+        self._upload_event = None
+        if self._async:
+            self._upload_event = torch.cuda.Event()
+            self._upload_event.record()
+
+    def wait_upload(self) -> None:
+        """Block until an asynchronous upload has landed (no-op for synchronous ones)."""
+        ev = getattr(self, '_upload_event', None)
+        if ev is not None:
+            ev.synchronize()
+            self._upload_event = None
 
     def _soa(self, torch, rowmajor: np.ndarray):
         # page-locked host arrays (thinning._host_buffer) go up asynchronously on the current stream:
         # the caller keeps them alive (SteinIntegrand holds them) and the layout kernel is queued
         # behind the copy, so host work after this call (the 'med' preconditioner) overlaps the DMA
         src = torch.from_numpy(rowmajor)
-        rm = src.to(self.device, non_blocking=bool(src.is_pinned()))
+        pinned = bool(src.is_pinned())
+        self._async = getattr(self, '_async', False) or pinned
+        rm = src.to(self.device, non_blocking=pinned)
         soa = torch.zeros((self.d, self.ld), dtype=torch.float64, device=self.device)
         nat.check(nat.lib().st_layout_soa(nat.ptr(rm), self.n, self.d, self.ld, nat.ptr(soa),
                                           nat.stream_handle()), 'st_layout_soa')

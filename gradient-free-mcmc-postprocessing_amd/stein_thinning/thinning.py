@@ -231,6 +231,9 @@ def _early_upload(sample: np.ndarray, gradient: np.ndarray, weights: Optional[np
 def _attach(integrand: SteinIntegrand, prob) -> SteinIntegrand:
     if prob is not None:
         prob.l, prob.tr = float(integrand.linv_scale), float(integrand.linv_trace)
+        # the preconditioner took longer than the DMA: this normally returns at once, and it keeps
+        # the integrand safe to use from any stream afterwards
+        prob.wait_upload()
         integrand._problem = prob
     return integrand
 
