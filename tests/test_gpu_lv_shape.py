@@ -42,3 +42,30 @@ def test_lv_call_shape_10000_points(shape):
     bad = np.flatnonzero(idx != want)
     assert bad.size == 0, f'{bad.size} of {M} indices differ from the C bit model; first at step {bad[0]}'
     np.testing.assert_array_equal(idx[:50], o.thin(sample, grads, 50, preconditioner='med'))
+
+
+def test_lv_gaussian_thin_call_shape_10000_points():
+    """The gradient-free LV call (``Gradient_free.ipynb`` cell 37, json :875-881): per chain
+    ``gaussian_thin(sample, log_p, np.mean(sample, 0), np.cov(sample, rowvar=False, ddof=d), 10_000)``
+    -- code/src/thinning.py:14-17, i.e. thin_gf with the Gaussian proxy, range_cap=200 and 'med' -- on
+    the 5e5-row log-space surrogate chain.  The GPU's proxy (log q, grad log q) feeds both sides: all
+    10 000 indices equal the C bit model on the same weights, and the first 50 equal the scipy-fed
+    NumPy oracle of the whole call (oracle/proxy_numpy.py)."""
+    import warnings
+    from bench import lv_surrogate
+    from oracle import proxy_numpy as op
+    from stein_thinning import proxy
+    s, _, log_p, _ = lv_surrogate(N, 12350, chain_len=N)
+    mean = np.mean(s, axis=0)
+    cov = np.cov(s, rowvar=False, ddof=s.shape[1])
+    with warnings.catch_warnings():
+        warnings.simplefilter('ignore')
+        idx = proxy.gaussian_thin(s, log_p, mean, cov, M)
+        log_q, gq = proxy.gaussian_proxy(s, mean, cov)
+        integrand = st._make_stein_gf_integrand(s, log_p, log_q, gq, range_cap=200, preconditioner='med')
+        head = op.gaussian_thin(s, log_p, mean, cov, 50)
+    want, _ = oracle_c.greedy_mt(integrand.sample, integrand.gradient, integrand.weights, integrand.linv_scale,
+                                 integrand.linv_trace, M, arith=nat.arithmetic())
+    bad = np.flatnonzero(idx != want)
+    assert bad.size == 0, f'{bad.size} of {M} indices differ from the C bit model; first at step {bad[0]}'
+    np.testing.assert_array_equal(idx[:50], head)
