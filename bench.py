@@ -251,6 +251,44 @@ def kernel_timing(prob, n_points: int, repeats: int = 5):
     return float(np.mean(per)), float(np.median(per))
 
 
+def dedup_timing(prob, m: int, want_idx, stream, repeats: int = 5):
+    """The drop-in thin's repeated-row path on the resident problem (DeviceProblem.dedup_view; not
+    `value`, which evaluates all n m pairs): run detection + compaction timed with the host clock
+    around a synchronised call (second of two, caches reset), then the thin of the run starts timed
+    with HIP events like the headline run, and whether its mapped-back indices equal the timed run's."""
+    import torch
+    det = []
+    for _ in range(2):
+        prob._dedup = False
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        view = prob.dedup_view()
+        torch.cuda.synchronize()
+        det.append(time.perf_counter() - t0)
+    if view is None:
+        return {'rows_kept': prob.n, 'of': prob.n, 'used': False, 'detect_s': round(det[-1], 6),
+                'note': 'fewer than 10 % of the rows repeat their predecessor: the drop-in thin evaluates all rows'}
+    sp = view.problem
+    idx, a, ws = sp.greedy_buffers(m)
+    sp.greedy_launch(m, idx, a, ws)
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(repeats)]
+    for e0, e1 in evs:
+        e0.record(stream)
+        sp.greedy_launch(m, idx, a, ws)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    med = float(np.median([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
+    got = view.to_rows(idx.cpu().numpy().view(np.uint32))
+    return {'used': True, 'drop_in_takes_it': bool(prob.dedup_pays(m) and prob.dedup_pays(m, sp.n)),
+            'rows_kept': sp.n, 'of': prob.n, 'detect_s': round(det[-1], 6),
+            'thin_s': round(med, 6), 's_per_thin_incl_detect': det[-1] + med,
+            'pair_evals_per_thin': sp.n * m,
+            'same_indices_as_timed_run': bool(np.array_equal(got, want_idx)),
+            'note': 'rows that repeat their predecessor bit for bit (rejected MCMC proposals) tie with their run '
+                    'start in every evaluation and lose the tie to its lower index, so the thin of the run '
+                    'starts selects the same rows (stein_thinning.device.DeviceProblem.dedup_view)'}
+
+
 # Rehearsal mode (ST_BENCH_SHARE_DEVICE=1, never used by the driver): every rank on cuda:0 and a
 # gloo group, so the N > 1 flow (mailbox setup, device exchange, timing reductions) can run on a
 # one-GPU box with several processes sharing the device.
@@ -539,16 +577,23 @@ def main():
                 stein_thinning.set_arithmetic('compact')
                 run_once()   # leave the buffers as the timed (compact) run left them
                 torch.cuda.synchronize()
+        dedup = None
+        if world == 1 and not sharded:
+            dedup = dedup_timing(prob, m, result_idx, stream)
         e2e = None
         if world == 1 and not cfg['gf'] and not cfg.get('d50'):
             # the drop-in call on host arrays (not `value`): standardisation + 'med' + H2D upload +
             # SoA layout + the persistent launch + D2H of the indices
             from stein_thinning import thinning as st
             st.thin(host_x, host_g, m, preconditioner='med')
-            t_e = time.perf_counter()
-            e2e_idx = st.thin(host_x, host_g, m, preconditioner='med')
-            dt_e = time.perf_counter() - t_e
-            e2e = {'thin_host_arrays_s': round(dt_e, 4), 'pair_evals_per_s': n * m / dt_e,
+            dts = []
+            for _ in range(3):
+                t_e = time.perf_counter()
+                e2e_idx = st.thin(host_x, host_g, m, preconditioner='med')
+                dts.append(time.perf_counter() - t_e)
+            dt_e = float(np.median(dts))
+            e2e = {'thin_host_arrays_s': round(dt_e, 4), 'runs_s': [round(v, 4) for v in dts],
+                   'pair_evals_per_s': n * m / dt_e,
                    'same_indices_as_timed_run': bool(np.array_equal(e2e_idx, result_idx))}
 
     exchange, degraded = None, False
@@ -586,11 +631,16 @@ def main():
                        'arithmetic': arithmetic if d <= 8 else 'exact',
                        'wallclock_thin_s': {
                            'device_resident': elapsed / args.steps,
+                           'device_resident_dedup': (round(dedup['s_per_thin_incl_detect'], 6)
+                                                     if rank == 0 and dedup else None),
                            'thin_host_arrays': e2e['thin_host_arrays_s'] if rank == 0 and e2e else None,
                            'note': 'device_resident = ms_per_step: the timed thin of the standardised sample '
-                                   'already in HBM (value); thin_host_arrays = the drop-in thin(sample, gradient, '
-                                   'm) on host NumPy arrays (validation, standardisation, med, H2D, launch, D2H), '
-                                   'timed once after the timed region'},
+                                   'already in HBM, every one of the n m pairs evaluated (value); '
+                                   'device_resident_dedup = the same thin with repeated rows dropped first '
+                                   '(run detection + compaction + the thin of the run starts: the drop-in '
+                                   'thin\'s default, same indices; "dedup" below); thin_host_arrays = the drop-in '
+                                   'thin(sample, gradient, m) on host NumPy arrays (validation, standardisation, '
+                                   'med, H2D, dedup, launch, D2H), timed once after the timed region'},
                        'first_indices': result_idx[:8].tolist()},
             'exchange': exchange,
             'degraded': degraded,
@@ -598,6 +648,7 @@ def main():
             'cpu_baseline': cpu,
             'end_to_end': e2e if rank == 0 and not sharded else None,
             'exact_arithmetic': exact if rank == 0 and not sharded else None,
+            'dedup': dedup if rank == 0 and not sharded else None,
         }
         print(json.dumps(line), flush=True)
     if sharded:

@@ -613,4 +613,47 @@ int st_layout_soa(const double* rowmajor, int64_t n, int32_t d, int64_t ld, doub
                      "layout launch");
 }
 
+// workspace of st_run_starts / st_run_compact: [0, 8) the run count (int64), then the per-tile
+// counts and offsets (int32 each)
+int64_t st_run_workspace_bytes(int64_t n) {
+    if (n < 1) return 16;
+    return (8 + 8 * st::run_tiles(n) + 15) / 16 * 16;
+}
+
+int st_run_starts(const double* x_soa, const double* g_soa, const double* weights, int64_t n, int32_t d,
+                  int64_t ld, uint8_t* starts_out, void* workspace, int64_t workspace_bytes, void* stream) {
+    int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
+    if (rc) return rc;
+    if (n > 0x7FFFFFFFll) return fail(ST_ERR_UNSUPPORTED, "n >= 2^31 rows");
+    if (!starts_out || !workspace) return fail(ST_ERR_INVALID, "NULL output/workspace");
+    if (!aligned16(workspace)) return fail(ST_ERR_INVALID, "workspace must be 16-byte aligned");
+    if (workspace_bytes < st_run_workspace_bytes(n))
+        return fail(ST_ERR_INVALID, "workspace too small (%lld < %lld)", (long long)workspace_bytes,
+                    (long long)st_run_workspace_bytes(n));
+    int64_t* count = static_cast<int64_t*>(workspace);
+    int32_t* tile_count = reinterpret_cast<int32_t*>(count + 1);
+    int32_t* tile_off = tile_count + st::run_tiles(n);
+    return hip_check(st::launch_run_starts(x_soa, g_soa, weights, n, d, ld, starts_out, tile_count, tile_off,
+                                           count, static_cast<hipStream_t>(stream)),
+                     "run-start launch");
+}
+
+int st_run_compact(const double* x_soa, const double* g_soa, const double* weights, int64_t n, int32_t d,
+                   int64_t ld, const uint8_t* starts, const void* workspace, int64_t count, int64_t ld_out,
+                   double* x_out, double* g_out, double* w_out, int32_t* rows_out, void* stream) {
+    int rc = check_problem(x_soa, g_soa, weights, n, d, ld);
+    if (rc) return rc;
+    if (n > 0x7FFFFFFFll) return fail(ST_ERR_UNSUPPORTED, "n >= 2^31 rows");
+    if (!starts || !workspace || !x_out || !g_out || !rows_out || (weights && !w_out))
+        return fail(ST_ERR_INVALID, "NULL input/output");
+    if (count < 1 || count > n || ld_out < count || (ld_out & 7))
+        return fail(ST_ERR_INVALID, "need 1 <= count <= n and ld_out >= count, a multiple of 8");
+    const int32_t* tile_off = reinterpret_cast<const int32_t*>(static_cast<const int64_t*>(workspace) + 1) +
+                              st::run_tiles(n);
+    return hip_check(st::launch_run_compact(x_soa, g_soa, weights, n, d, ld, starts, tile_off, count, ld_out,
+                                            x_out, g_out, weights ? w_out : nullptr, rows_out,
+                                            static_cast<hipStream_t>(stream)),
+                     "run-compact launch");
+}
+
 }  // extern "C"

@@ -154,5 +154,13 @@ hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, cons
                                   double* out, double* ws, int64_t ws_doubles, hipStream_t s);
 hipError_t launch_layout_soa(const double* rowmajor, int64_t n, int d, int64_t ld, double* soa,
                              hipStream_t s);
+// repeated-row compaction (dedup.hip)
+int64_t run_tiles(int64_t n);
+hipError_t launch_run_starts(const double* x, const double* g, const double* w, int64_t n, int d, int64_t ld,
+                             uint8_t* starts, int32_t* tile_count, int32_t* tile_off, int64_t* count,
+                             hipStream_t s);
+hipError_t launch_run_compact(const double* x, const double* g, const double* w, int64_t n, int d, int64_t ld,
+                              const uint8_t* starts, const int32_t* tile_off, int64_t count, int64_t ld_out,
+                              double* xo, double* go, double* wo, int32_t* rows_out, hipStream_t s);
 
 }  // namespace st

@@ -16,10 +16,53 @@ import numpy as np
 from . import _native as nat
 
 PAD = 64
+# thin the run starts instead of all rows when at most this fraction of the rows start a run ...
+DEDUP_MAX_FRAC = 0.9
+# ... and (greedy(dedup=True)) the pair work it saves is estimated at >= this many seconds
+DEDUP_MIN_SAVING_S = 50e-6
 
 
 def padded_ld(n: int) -> int:
     return max(PAD, ((n + PAD - 1) // PAD) * PAD)
+
+
+class DedupView:
+    """A problem's run starts as a compact DeviceProblem (DeviceProblem.dedup_view) and the maps
+    between the two index spaces (the compaction keeps row order, so a lower index stays lower)."""
+
+    def __init__(self, parent: 'DeviceProblem', starts, ws, count: int):
+        import torch
+        d, dev = parent.d, parent.device
+        ld = padded_ld(count)
+        x = torch.empty((d, ld), dtype=torch.float64, device=dev)
+        g = torch.empty((d, ld), dtype=torch.float64, device=dev)
+        w = torch.empty(ld, dtype=torch.float64, device=dev) if parent.w is not None else None
+        self.rows = torch.empty(count, dtype=torch.int32, device=dev)   # compact row -> source row
+        nat.check(nat.lib().st_run_compact(
+            nat.ptr(parent.x), nat.ptr(parent.g), nat.ptr(parent.w), parent.n, d, parent.ld, nat.ptr(starts),
+            nat.ptr(ws), count, ld, nat.ptr(x), nat.ptr(g), nat.ptr(w), nat.ptr(self.rows),
+            nat.stream_handle()), 'st_run_compact')
+        self.starts = starts                                   # (n,) uint8: row starts a run
+        self.problem = DeviceProblem.from_soa(x, g, w, count, parent.l, parent.tr)
+
+    @property
+    def n_unique(self) -> int:
+        return self.problem.n
+
+    @property
+    def rows_host(self) -> np.ndarray:
+        return self.rows.cpu().numpy().astype(np.uint32)
+
+    def to_rows(self, compact_idx: np.ndarray) -> np.ndarray:
+        import torch
+        t = torch.from_numpy(np.asarray(compact_idx, dtype=np.int64)).to(self.rows.device)
+        return self.rows.index_select(0, t).cpu().numpy().astype(np.uint32)
+
+    def expand_sums(self, a_compact) -> np.ndarray:
+        """Running sums of all parent rows: every row takes its run start's."""
+        import torch
+        group = torch.cumsum(self.starts, 0, dtype=torch.int64) - 1
+        return a_compact.index_select(0, group).cpu().numpy()
 
 
 def isotropic_scale(linv: np.ndarray):
@@ -118,16 +161,35 @@ class DeviceProblem:
             self.l, self.tr, 0, int(n_points), int(n_points), nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
             ws.numel() * 8, nat.stream_handle()), 'st_greedy_steps')
 
-    def greedy(self, n_points: int, return_sums: bool = False, margins: bool = False):
+    def greedy(self, n_points: int, return_sums: bool = False, margins: bool = False, dedup=False):
         """The reference's _greedy_search on the device.  ``self.fallback`` is None when the
         persistent launch completed, else why the run was repeated on the launch-per-step path
         (its bounded waits expired: the grid was not co-resident next to other work).
         ``margins=True``: (indices, diagnostics.GreedyMargins) -- the same selection with each step's
-        argmin margin against the arithmetic's error band (launch-per-step kernels, one step at a time)."""
+        argmin margin against the arithmetic's error band (launch-per-step kernels, one step at a time).
+        ``dedup=True``: thin the run starts only (``dedup_view``) when repeated rows make that
+        worthwhile (``dedup_pays``); ``dedup='always'``: whenever dedup_view has a view.  Either way
+        the same indices and running sums bit for bit."""
         if margins:
             from .diagnostics import greedy_margins
             gm = greedy_margins(self, n_points)
             return gm.indices, gm
+        view = None
+        if dedup == 'always' or (dedup and self.dedup_pays(n_points)):
+            view = self.dedup_view()
+            if view is not None and dedup != 'always' and not self.dedup_pays(n_points, view.n_unique):
+                view = None
+        self.dedup_used = view is not None
+        if view is not None:
+            out, a = view.problem._greedy_run(n_points)
+            self.fallback = view.problem.fallback
+            out = view.to_rows(out)
+            return (out, view.expand_sums(a)) if return_sums else out
+        out, a = self._greedy_run(n_points)
+        return (out, a[:self.n].cpu().numpy()) if return_sums else out
+
+    def _greedy_run(self, n_points: int):
+        """(uint32 indices on the host, running sums on the device)."""
         idx, a, ws = self.greedy_buffers(n_points)
         self.greedy_launch(n_points, idx, a, ws)
         out = idx.cpu().numpy().view(np.uint32).copy()
@@ -135,14 +197,56 @@ class DeviceProblem:
         if out.size and int(out.max()) >= self.n:
             self.fallback = ('persistent greedy kernel timed out (grid not co-resident?); '
                              're-ran on the launch-per-step kernels')
-            warnings.warn(self.fallback, RuntimeWarning, stacklevel=2)
+            warnings.warn(self.fallback, RuntimeWarning, stacklevel=3)
             self.greedy_steps_launch(n_points, idx, a, ws)
             out = idx.cpu().numpy().view(np.uint32).copy()
             if out.size and int(out.max()) >= self.n:
                 raise nat.HipExtensionError('greedy step kernels returned out-of-range indices')
-        if return_sums:
-            return out, a[:self.n].cpu().numpy()
-        return out
+        return out, a
+
+    def dedup_view(self) -> Optional['DedupView']:
+        """The run starts of this problem as a compact problem, or None when fewer than
+        ``1 - DEDUP_MAX_FRAC`` of the rows repeat their predecessor (computed once, then cached).
+
+        A row that repeats the row before it bit for bit (x, g and w: a rejected MCMC proposal;
+        about 77 % of the rows of a random-walk chain at the usual acceptance rate) has every pair
+        value, hence every running sum, equal to the run's first row, so it can only tie with that
+        row and lose the tie to its lower index (np.argmin order): it is never selected.  Thinning
+        the run starts and mapping the winners back gives the same indices, and the dropped rows'
+        sums are their run start's."""
+        import torch
+        cached = getattr(self, '_dedup', False)
+        if cached is not False:
+            return cached
+        view = None
+        if self.n > 1:
+            L = nat.lib()
+            starts = torch.empty(self.n, dtype=torch.uint8, device=self.device)
+            ws = torch.empty((int(L.st_run_workspace_bytes(self.n)) + 7) // 8, dtype=torch.int64, device=self.device)
+            nat.check(L.st_run_starts(nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.n, self.d, self.ld,
+                                      nat.ptr(starts), nat.ptr(ws), ws.numel() * 8, nat.stream_handle()),
+                      'st_run_starts')
+            count = int(ws[0].item())   # sizes the compact arrays
+            if count <= DEDUP_MAX_FRAC * self.n:
+                view = DedupView(self, starts, ws, count)
+        self._dedup = view
+        return view
+
+    def dedup_pays(self, n_points: int, n_unique: Optional[int] = None) -> bool:
+        """Cost gate of ``greedy(dedup=True)`` (a heuristic: either answer gives the same indices).
+        Before detection (n_unique None): is the whole thin's pair work worth a detection pass
+        (>= 4 x DEDUP_MIN_SAVING_S)?  After: do the dropped rows save >= DEDUP_MIN_SAVING_S?  Per-pair
+        costs measured on MI355X: ~1.8 ps per Langevin d = 4 pair on the
+        persistent kernel above its per-step exchange floor, scaled by the flop count for d <= 8;
+        the launch-per-step kernels of d > 8 stream (16 d + 24) B per pair at ~5 TB/s."""
+        d = self.d
+        if d <= 8:
+            per_pair = 1.8e-12 * (12 * d + 40 + (2 if self.w is not None else 0)) / 88.0
+        else:
+            per_pair = (16 * d + 24) / 5e12
+        if n_unique is None:
+            return self.n * n_points * per_pair >= 4 * DEDUP_MIN_SAVING_S
+        return (self.n - n_unique) * n_points * per_pair >= DEDUP_MIN_SAVING_S
 
     # -- integrand protocol --------------------------------------------------------------------
     def pairs(self, i1: np.ndarray, i2: np.ndarray) -> np.ndarray:
@@ -168,10 +272,12 @@ class DeviceProblem:
     def subset(self, rows: np.ndarray) -> 'DeviceProblem':
         """Compact problem of the given rows (gather on device; used by ksd / kmat)."""
         import torch
-        rows = np.asarray(rows, dtype=np.int64).reshape(-1)
-        m = rows.shape[0]
+        if isinstance(rows, torch.Tensor):
+            ti = rows.to(device=self.device, dtype=torch.int64).reshape(-1)
+        else:
+            ti = torch.from_numpy(np.asarray(rows, dtype=np.int64).reshape(-1)).to(self.device)
+        m = int(ti.shape[0])
         ld = padded_ld(m)
-        ti = torch.from_numpy(rows).to(self.device)
         x = torch.zeros((self.d, ld), dtype=torch.float64, device=self.device)
         g = torch.zeros((self.d, ld), dtype=torch.float64, device=self.device)
         x[:, :m] = self.x.index_select(1, ti)

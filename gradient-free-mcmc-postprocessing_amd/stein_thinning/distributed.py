@@ -671,10 +671,19 @@ def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None
     rank, world = _world(group)
     if world > integrand.n:
         raise ValueError(f'{world} ranks for {integrand.n} rows: every rank needs at least one row')
+    from .thinning import _dedup
+    view = integrand.run_starts_view() if _dedup() else None
+    rows = None
+    if view is not None and view[0].n >= world:
+        integrand, rows = view   # the run starts only (thinning.set_dedup; same indices)
+    if world > 1 and not _group_same(np.array([-1 if rows is None else rows.size], dtype=np.int64), group):
+        raise ValueError('sharded thin: the ranks disagree on the repeated-row path '
+                         '(stein_thinning.set_dedup / ST_DEDUP must agree, and so must the sample)')
     global last_mode
     runner = sharded_runner(integrand, n_points, group, use_graph)
     last_mode = runner.mode
-    return runner.indices()
+    idx = runner.indices()
+    return idx if rows is None else rows[idx.astype(np.int64)].astype(np.uint32)
 
 
 last_mode = None   # exchange engine of the last sharded thin in this process (tests / bench)

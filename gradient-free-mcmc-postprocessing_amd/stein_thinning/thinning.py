@@ -179,6 +179,24 @@ class SteinIntegrand:
     def base_problem(self):
         return self.base().device_problem()
 
+    def run_starts_view(self):
+        """(compact integrand of the run starts, their rows) on the host arrays, or None when the
+        repeated-row path does not pay (device.DeviceProblem.dedup_view's rule and reasoning; used by
+        the row-sharded thin, which builds every rank's shard from the host arrays)."""
+        from .device import DEDUP_MAX_FRAC
+        if self._base is not None or self.n < 2:
+            return None
+        cols = [self.sample, self.gradient] + ([self.weights.reshape(-1, 1)] if self.weights is not None else [])
+        diff = np.zeros(self.n - 1, dtype=bool)
+        for c in cols:
+            u = np.ascontiguousarray(c).view(np.uint64)
+            diff |= (u[1:] != u[:-1]).any(axis=1)
+        rows = np.concatenate([[0], 1 + np.flatnonzero(diff)])
+        if rows.size > DEDUP_MAX_FRAC * self.n:
+            return None
+        w = self.weights[rows] if self.weights is not None else None
+        return SteinIntegrand(self.sample[rows], self.gradient[rows], self.linv, w), rows
+
     def device_problem(self):
         if self._problem is None:
             if self._base is not None:
@@ -321,8 +339,24 @@ def _greedy_search(n_points: int, integrand: Callable) -> np.ndarray:
         if integrand._base is None and _rank_sharding():
             from .distributed import thin_across_ranks
             return thin_across_ranks(integrand, n_points)
-        return integrand.device_problem().greedy(n_points)
+        return integrand.device_problem().greedy(n_points, dedup=_dedup())
     return _greedy_search_protocol(n_points, integrand)
+
+
+_DEDUP = None
+
+
+def set_dedup(enabled: Optional[bool]) -> None:
+    """Thin only the first row of each run of repeated rows (DeviceProblem.dedup_view: the same
+    indices bit for bit, a fraction of the pair work on MCMC output full of rejected proposals):
+    True / False, or None to return to the ST_DEDUP environment variable ('0' = off; on by default)."""
+    global _DEDUP
+    _DEDUP = None if enabled is None else bool(enabled)
+
+
+def _dedup() -> bool:
+    import os
+    return _DEDUP if _DEDUP is not None else os.environ.get('ST_DEDUP', '1') != '0'
 
 
 def thin(sample, gradient, n_points: int, standardize: bool = True, preconditioner='id') -> np.ndarray:

@@ -336,6 +336,26 @@ int st_standardize_host(const double *sample, const double *gradient, int64_t n,
                         int32_t standardize, double *sample_out, double *gradient_out,
                         double *loc_out, double *scl_out, int32_t *status);
 
+/* ------------------------------------------------------------------------------------------
+ * Repeated-row compaction (stein_thinning.device.DeviceProblem.dedup_view; no reference
+ * counterpart -- an exact shortcut in front of st_greedy).  A row equal bit for bit (x, g, w) to the
+ * row before it ties with its run's first row at every step of _greedy_search
+ * (JAX_Stein_Thinning.ipynb:281-295) and loses the tie to the lower index, so st_greedy on the run
+ * starts, mapped back through rows_out, returns the same indices.
+ *   st_run_starts:  starts_out[i] = 1 iff row i starts a run (n bytes); the number of runs lands in
+ *                   the first 8 bytes of `workspace` (int64; st_run_workspace_bytes(n), 16-B aligned);
+ *   st_run_compact: after the caller read that count: the run starts into (d, ld_out) SoA arrays
+ *                   x_out / g_out (and w_out when weights is non-NULL) in row order, rows_out[k] = the
+ *                   source row of compact row k (int32), rows [count, ld_out) zeroed.
+ * n < 2^31.  Same stream for both calls.
+ * ---------------------------------------------------------------------------------------- */
+int64_t st_run_workspace_bytes(int64_t n);
+int st_run_starts(const double *x_soa, const double *g_soa, const double *weights, int64_t n, int32_t d,
+                  int64_t ld, uint8_t *starts_out, void *workspace, int64_t workspace_bytes, void *stream);
+int st_run_compact(const double *x_soa, const double *g_soa, const double *weights, int64_t n, int32_t d,
+                   int64_t ld, const uint8_t *starts, const void *workspace, int64_t count, int64_t ld_out,
+                   double *x_out, double *g_out, double *w_out, int32_t *rows_out, void *stream);
+
 /* row-major (n, d) -> SoA (d, ld) layout helper (device to device) */
 int st_layout_soa(const double *rowmajor, int64_t n, int32_t d, int64_t ld, double *soa,
                   void *stream);

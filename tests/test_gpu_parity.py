@@ -487,6 +487,11 @@ def test_config4_full_length_bit_exact(config4):
     idx, A = prob.greedy(c['m'], return_sums=True)
     np.testing.assert_array_equal(idx, c['idx'])
     assert np.array_equal(A, c['A']), np.flatnonzero(A != c['A'])[:10]
+    # the repeated-row path (the drop-in thin's default): 24 % of the rows start a run
+    didx, dA = prob.greedy(c['m'], return_sums=True, dedup=True)
+    assert prob.dedup_used and prob.dedup_view().n_unique < 0.3 * prob.n
+    np.testing.assert_array_equal(didx, c['idx'])
+    assert np.array_equal(dA, c['A']), np.flatnonzero(dA != c['A'])[:10]
     np.testing.assert_array_equal(st.thin(c['x'], c['g'], c['m'], preconditioner='med'), c['idx'])
 
 

@@ -1,7 +1,8 @@
 """Persistent-kernel variant sweep on one GPU: time st_greedy for the bench configs under several
 st_tune settings and check that every variant selects the same indices.
 
-    python tools/tune_sweep.py [c4|c2|c3|c4@<n>] "8=1" "8=2" "8=2,3=4" ...
+    python tools/tune_sweep.py [c4|c2|c3|c4@<n>][+dedup] "8=1" "8=2" "8=2,3=4" ...
+(+dedup: the thin of the run starts, DeviceProblem.dedup_view, as the drop-in thin runs it)
 Each argument is a comma-separated list of key=value st_tune settings (reset to -1 between)."""
 import os
 import sys
@@ -19,12 +20,16 @@ from stein_thinning import _native as nat  # noqa: E402
 cfg_name = sys.argv[1] if len(sys.argv) > 1 and not '=' in sys.argv[1] else 'c4'
 settings = [a for a in sys.argv[1:] if '=' in a] or ['8=1', '8=2']
 # "c4@1000000": config 4's data and m at another n (crossover sweeps)
+cfg_name, plus, mode = cfg_name.partition('+')
 base, _, n_over = cfg_name.partition('@')
 cfg = dict(bench.CONFIGS[base])
 if n_over:
     cfg['n'] = int(float(n_over))
 integrand, _, _ = bench.make_integrand(cfg)
 prob = integrand.device_problem()
+if mode == 'dedup':
+    prob = prob.dedup_view().problem
+    print(f'{cfg_name}+dedup: {prob.n} run starts of {cfg["n"]} rows', flush=True)
 m = cfg['m']
 L = nat.lib()
 ref = None
