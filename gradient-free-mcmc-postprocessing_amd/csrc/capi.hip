@@ -613,6 +613,13 @@ int st_layout_soa(const double* rowmajor, int64_t n, int32_t d, int64_t ld, doub
                      "layout launch");
 }
 
+int st_pdist(const double* rows, int64_t k, int32_t d, double* out, void* stream) {
+    if (!rows || !out) return fail(ST_ERR_INVALID, "NULL pointer");
+    if (k < 2 || k > 65535 || d < 1 || d > st::kMaxDim)
+        return fail(ST_ERR_INVALID, "need 2 <= k <= 65535 rows and 1 <= d <= %d", st::kMaxDim);
+    return hip_check(st::launch_pdist(rows, k, d, out, static_cast<hipStream_t>(stream)), "pdist launch");
+}
+
 // workspace of st_run_starts / st_run_compact: [0, 8) the run count (int64), then the per-tile
 // counts and offsets (int32 each)
 int64_t st_run_workspace_bytes(int64_t n) {

@@ -65,6 +65,25 @@ class DedupView:
         return a_compact.index_select(0, group).cpu().numpy()
 
 
+def pdist_median(sub: np.ndarray, device=None) -> np.float64:
+    """np.median(scipy.spatial.distance.pdist(sub)) with the distances computed and sorted on the
+    GPU (st_pdist: bit-identical to scipy's) on a side stream, so it runs while a large upload is in
+    flight on the current one; the middle value(s) come back and are averaged by np.mean exactly as
+    np.median averages them.  ``sub``: (k, d) host rows, 2 <= k <= 65535."""
+    import torch
+    dev = device if device is not None else nat.require_device()
+    sub = np.ascontiguousarray(sub, dtype=np.float64)
+    k, d = sub.shape
+    cnt = k * (k - 1) // 2
+    side = torch.cuda.Stream(device=dev)
+    with torch.cuda.stream(side):
+        rows = torch.from_numpy(sub).to(dev)
+        dist = torch.empty(cnt, dtype=torch.float64, device=dev)
+        nat.check(nat.lib().st_pdist(nat.ptr(rows), k, d, nat.ptr(dist), nat.stream_handle()), 'st_pdist')
+        mid = torch.sort(dist).values[(cnt - 1) // 2:cnt // 2 + 1].cpu().numpy()
+    return np.mean(mid)
+
+
 def isotropic_scale(linv: np.ndarray):
     """(l, trace) if linv == l * I exactly, else None (dense preconditioners: not on the HIP path)."""
     linv = np.asarray(linv, dtype=np.float64)

@@ -17,19 +17,24 @@ from scipy.spatial.distance import pdist
 MED_SUBSAMPLE = 1000
 
 
-def make_precon(sample: np.ndarray, preconditioner='id') -> np.ndarray:
+def make_precon(sample: np.ndarray, preconditioner='id', on_device: bool = False) -> np.ndarray:
     """Gamma^-1 for the IMQ kernel (reference usage: ``make_precon(s, 'id')``,
     ``JAX_Stein_Thinning.ipynb`` cell 28; median heuristic ``report.tex:432``).
 
     'id' -> I; 'med' -> inv(med^2 I), med = median pairwise distance of the (standardised) sample,
     sub-sampled at ``linspace(0, n-1, 1000)`` rows when n > 1000 (sub-sampling rule: parity
     unpinned); 'sclmed' -> inv(med^2 / log(min(1000, n)) I); a number s -> inv(s I).
+    ``on_device``: the median's distances computed and sorted on the GPU (device.pdist_median, the
+    same bits; the drop-in thin's path, which holds the GPU anyway) instead of scipy + np.median.
     """
     sample = np.asarray(sample, dtype=np.float64)
     n, d = sample.shape
 
     def med2():
         sub = sample[np.linspace(0, n - 1, MED_SUBSAMPLE, dtype=int)] if n > MED_SUBSAMPLE else sample
+        if on_device and 2 <= sub.shape[0] <= 65535:
+            from .device import pdist_median
+            return pdist_median(sub) ** 2
         return np.median(pdist(sub)) ** 2
 
     if isinstance(preconditioner, str):

@@ -259,7 +259,7 @@ def _attach(integrand: SteinIntegrand, prob) -> SteinIntegrand:
 def _make_stein_integrand(sample, gradient, standardize: bool = True, preconditioner='id') -> SteinIntegrand:
     sample, gradient = _validate_and_standardize(sample, gradient, standardize)
     prob = _early_upload(sample, gradient, None) if preconditioner == 'med' else None
-    linv = make_precon(sample, preconditioner)
+    linv = make_precon(sample, preconditioner, on_device=prob is not None)
     return _attach(SteinIntegrand(sample, gradient, linv), prob)
 
 
@@ -275,7 +275,7 @@ def _make_stein_gf_integrand(sample, log_p, log_q, gradient_q, standardize: bool
         raise ValueError('log_p or log_q contains NaNs.')
     weights = np.exp(_log_weights(log_p, log_q, range_cap))
     prob = _early_upload(sample, gradient_q, weights) if preconditioner == 'med' else None
-    linv = make_precon(sample, preconditioner)
+    linv = make_precon(sample, preconditioner, on_device=prob is not None)
     return _attach(SteinIntegrand(sample, gradient_q, linv, weights), prob)
 
 

@@ -336,6 +336,12 @@ int st_standardize_host(const double *sample, const double *gradient, int64_t n,
                         int32_t standardize, double *sample_out, double *gradient_out,
                         double *loc_out, double *scl_out, int32_t *status);
 
+/* scipy.spatial.distance.pdist(rows) (euclidean) of row-major (k, d) device rows into out
+ * (k (k - 1) / 2 doubles, scipy's condensed order), bit-identical to scipy 1.15: the 'med'
+ * preconditioner's median heuristic (stein_thinning.kernel.make_precon, report.tex:432) sorts them on
+ * the device.  2 <= k <= 65535. */
+int st_pdist(const double *rows, int64_t k, int32_t d, double *out, void *stream);
+
 /* ------------------------------------------------------------------------------------------
  * Repeated-row compaction (stein_thinning.device.DeviceProblem.dedup_view; no reference
  * counterpart -- an exact shortcut in front of st_greedy).  A row equal bit for bit (x, g, w) to the
