@@ -379,6 +379,8 @@ def main():
     ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
     ap.add_argument('--lv-global-obs', type=int, default=0,
                     help='lv workload: 1 = phase B reads the observations from global memory (st_tune key 17)')
+    ap.add_argument('--lv-pieces', type=int, default=-1,
+                    help='lv workload: phase-B observation pieces per lane (st_tune key 18; -1 = auto)')
     ap.add_argument('--proxy-mode', type=int, default=0, help='proxy kernel (st_tune key 7; 0 = auto)')
     ap.add_argument('--energy-variant', type=int, default=0, help='energy kernel (st_tune key 13; 0 = auto)')
     ap.add_argument('--energy-units', type=int, default=-1,
@@ -1025,6 +1027,7 @@ def main_lv(args):
     L = nat.lib()
     two_phase = args.lv_mode == 0
     nat.check(L.st_tune(17, args.lv_global_obs), 'st_tune')
+    nat.check(L.st_tune(18, args.lv_pieces), 'st_tune')
     wb = int(L.st_lv_grad_workspace_bytes(m, t.size))
     work = torch.empty((wb + 7) // 8, dtype=torch.float64, device=dev) if two_phase else None
 

@@ -86,6 +86,7 @@ int st_tune(int32_t key, int32_t value) {
     else if (key == 13) rc = st::dist_tune(value);
     else if (key == 14) rc = st::dist_units_tune(value);
     else if (key == 17) rc = st::lv_tune(value);
+    else if (key == 18) rc = st::lv_pieces_tune(value);
     else rc = ((key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12 || key == 15 || key == 16)
                   ? st::persistent_tune(key, value)
                                                                                           : st::tune(key, value);

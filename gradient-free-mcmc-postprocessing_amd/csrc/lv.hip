@@ -351,7 +351,7 @@ __device__ __forceinline__ int wave_sum_int(int v) {
 // with each lane of a wave at a different observation index, every t_eval / y_obs load touched 64
 // cache lines and the texture address unit was busy ~80 % of the kernel while the VALU issued on
 // ~60 % of SIMD cycles.
-template <int WPB, bool LDS>
+template <int WPB, bool LDS, int KP>
 __global__ __launch_bounds__(64 * WPB) void lv_dense_kernel(LvArgs a) {
     const int64_t i = (int64_t)blockIdx.x * WPB + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
@@ -376,14 +376,15 @@ __global__ __launch_bounds__(64 * WPB) void lv_dense_kernel(LvArgs a) {
         kb_s = (int)r[2];
         len = (int)r[3] - kb_s;
     }
-    // smallest P with sum_s ceil(len_s / P) <= 64 (ns <= 64 guarantees P = max len qualifies)
-    int plo = (a.t_n + 63) / 64, phi = len;
+    // smallest P with sum_s ceil(len_s / P) <= 64 KP (ns <= 64 guarantees P = max len qualifies)
+    constexpr int kPieces = 64 * KP;
+    int plo = (a.t_n + kPieces - 1) / kPieces, phi = len;
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) phi = max(phi, __shfl_xor(phi, off));
     if (plo > phi) plo = phi;
     while (plo < phi) {
         const int mid = (plo + phi) >> 1;
-        if (wave_sum_int((len + mid - 1) / mid) <= 64) phi = mid; else plo = mid + 1;
+        if (wave_sum_int((len + mid - 1) / mid) <= kPieces) phi = mid; else plo = mid + 1;
     }
     const int P = plo > 0 ? plo : 1;
     const int np = (len + P - 1) / P;
@@ -396,19 +397,27 @@ __global__ __launch_bounds__(64 * WPB) void lv_dense_kernel(LvArgs a) {
     pstart[lane + 1] = incl;
     if (lane == 0) pstart[0] = 0;
     __builtin_amdgcn_wave_barrier();
-    const int total = __shfl(incl, 63);   // <= 64
+    const int total = __shfl(incl, 63);   // <= 64 KP
     double acc[4] = {0.0, 0.0, 0.0, 0.0};
-    if (lane < total) {
-        int lo = 0, hi = ns - 1;           // step s with pstart[s] <= lane < pstart[s + 1]
+    const double c0 = a.cinv[0], c1 = a.cinv[1], c2 = a.cinv[2], c3 = a.cinv[3];
+    // KP pieces per lane, dealt in a snake (round u: lane L takes piece 64u + L, or 64u + 63 - L
+    // in odd rounds), so a lane whose first piece is a step's short remainder tends to get a long one
+    // next (round 4: KP = 2 cuts the busiest lane's share of a point from 1 / 0.75 of the even split
+    // to 1 / 0.86, tools/lv_piece_balance.py)
+#pragma unroll 1
+    for (int u = 0; u < KP; ++u) {
+        const int pc = 64 * u + ((u & 1) ? 63 - lane : lane);
+        if (pc >= total) continue;
+        int lo = 0, hi = ns - 1;           // step s with pstart[s] <= pc < pstart[s + 1]
         while (lo < hi) {
             const int mid = (lo + hi + 1) >> 1;
-            if (pstart[mid] <= lane) lo = mid; else hi = mid - 1;
+            if (pstart[mid] <= pc) lo = mid; else hi = mid - 1;
         }
         const double* r = tab + (int64_t)lo * kLvStepRec;
         const double2* r2 = reinterpret_cast<const double2*>(r);
         const double2 h0 = r2[0], h1 = r2[1];
         const double t_old = h0.x, inv_hd = h0.y;
-        const int kb = (int)h1.x + (lane - pstart[lo]) * P;
+        const int kb = (int)h1.x + (pc - pstart[lo]) * P;
 #if defined(ST_LV_DIAG) && ST_LV_DIAG == 1   // diagnostic build: preamble and record loads only
         const int ke = kb + 1;
 #else
@@ -429,7 +438,6 @@ __global__ __launch_bounds__(64 * WPB) void lv_dense_kernel(LvArgs a) {
         // the observation (t_k, y_k) loads of the next two points are in flight while this pair
         // computes (L2-served, shared by every parameter point: without the prefetch each
         // iteration waited a full load latency at three waves per SIMD); same order of the sums
-        const double c0 = a.cinv[0], c1 = a.cinv[1], c2 = a.cinv[2], c3 = a.cinv[3];
         auto obs = [&](int k, double& tk, double& o0, double& o1) {
             const int kc = k < ke ? k : ke - 1;    // past the piece: a harmless reload, unused
             if constexpr (LDS) {
@@ -496,6 +504,14 @@ int lv_tune(int value) {
     return 0;
 }
 
+// st_tune key 18: phase-B pieces per lane (1, 2, 3; -1 = automatic)
+static int g_lv_pieces = -1;
+int lv_pieces_tune(int value) {
+    if (value != -1 && (value < 1 || value > 3)) return -1;
+    g_lv_pieces = value;
+    return 0;
+}
+
 int64_t lv_grad_workspace_bytes(int64_t n, int step_cap) {
     return n * ((int64_t)step_cap * kLvStepRec * 8 + 8);
 }
@@ -510,10 +526,15 @@ hipError_t launch_lv(const LvArgs& a, bool gradient, hipStream_t s) {
         if (e != hipSuccess) return e;
         // observations in LDS when they fit the default 64 KB dynamic allocation (t_n <= 2730)
         const size_t obs_bytes = (size_t)a.t_n * 3 * sizeof(double);
-        if (obs_bytes <= 65536 && g_lv_global_obs != 1)
-            lv_dense_kernel<8, true><<<(unsigned)((a.n + 7) / 8), 512, obs_bytes, s>>>(a);
-        else
-            lv_dense_kernel<4, false><<<(unsigned)((a.n + 3) / 4), 256, 0, s>>>(a);
+        const int kp = g_lv_pieces > 0 ? g_lv_pieces : 1;
+        if (obs_bytes <= 65536 && g_lv_global_obs != 1) {
+            const unsigned nb = (unsigned)((a.n + 7) / 8);
+            if (kp == 2) lv_dense_kernel<8, true, 2><<<nb, 512, obs_bytes, s>>>(a);
+            else if (kp == 3) lv_dense_kernel<8, true, 3><<<nb, 512, obs_bytes, s>>>(a);
+            else lv_dense_kernel<8, true, 1><<<nb, 512, obs_bytes, s>>>(a);
+        } else {
+            lv_dense_kernel<4, false, 1><<<(unsigned)((a.n + 3) / 4), 256, 0, s>>>(a);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         lv_kernel<10, false, true><<<blocks, kLvThreads, 0, s>>>(a);
         return hipGetLastError();

@@ -149,6 +149,7 @@ hipError_t launch_ksd_finish(const PairArgs& p, int64_t n, const double* csum, d
 int64_t distance_chunks(int64_t na, int64_t b_begin, int64_t b_end);
 int dist_units_tune(int value);   // st_tune key 14
 int lv_tune(int value);           // st_tune key 17
+int lv_pieces_tune(int value);    // st_tune key 18
 hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, const double* b,
                                   int64_t ldb, int64_t b0, int64_t b1, int d, int tri,
                                   double* out, double* ws, int64_t ws_doubles, hipStream_t s);

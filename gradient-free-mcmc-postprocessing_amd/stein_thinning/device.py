@@ -65,6 +65,9 @@ class DedupView:
         return a_compact.index_select(0, group).cpu().numpy()
 
 
+_SIDE_STREAMS = {}   # device -> the side stream of pdist_median (one per process)
+
+
 def pdist_median(sub: np.ndarray, device=None) -> np.float64:
     """np.median(scipy.spatial.distance.pdist(sub)) with the distances computed and sorted on the
     GPU (st_pdist: bit-identical to scipy's) on a side stream, so it runs while a large upload is in
@@ -75,7 +78,9 @@ def pdist_median(sub: np.ndarray, device=None) -> np.float64:
     sub = np.ascontiguousarray(sub, dtype=np.float64)
     k, d = sub.shape
     cnt = k * (k - 1) // 2
-    side = torch.cuda.Stream(device=dev)
+    side = _SIDE_STREAMS.get(dev)
+    if side is None:
+        side = _SIDE_STREAMS[dev] = torch.cuda.Stream(device=dev)
     with torch.cuda.stream(side):
         rows = torch.from_numpy(sub).to(dev)
         dist = torch.empty(cnt, dtype=torch.float64, device=dev)

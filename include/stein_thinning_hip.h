@@ -86,7 +86,8 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * 0 otherwise;
  * timing only, same results), key 17 = LV gradient phase B: 1 reads the observation times / data
  * from global memory as round 3 did (0 / -1 = automatic: staged in LDS when 3 t_n doubles fit
- * 64 KB; same results).
+ * 64 KB; same results), key 18 = LV gradient phase B: observation pieces per lane (1, 2, 3; -1 =
+ * automatic; the per-point sum is reassociated differently, within the 1e-8 tolerance).
  */
 int st_tune(int32_t key, int32_t value);
 

@@ -47,7 +47,9 @@ def test_persistent_grid_not_coresident_falls_back():
     lib = ctypes.CDLL(HELPER)
     lib.st_test_occupy.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
     sink = torch.zeros(1, dtype=torch.int32, device='cuda')
-    side = torch.cuda.Stream()
+    # a high-priority stream: HIP gives it a hardware queue of its own (a normal-priority pool stream
+    # can share the default stream's queue, which would serialise the two kernels instead)
+    side = torch.cuda.Stream(priority=torch.cuda.Stream.priority_range()[1])
     # 64 CUs held for 0.4 s by blocks that take all of a CU's LDS: 64 of the persistent kernel's
     # one-block-per-CU grid (each ~160 KB of LDS at this n) cannot start until they leave
     assert lib.st_test_occupy(64, 163840, 40_000_000, ctypes.c_void_p(sink.data_ptr()),

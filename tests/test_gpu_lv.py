@@ -124,3 +124,23 @@ def test_two_phase_step_table_overflow_falls_back(data):
 def test_two_phase_chunks(data):
     th = _points(50, 0.05, 7)
     np.testing.assert_array_equal(lv.grad_log_posterior(th, data, chunk=7), lv.grad_log_posterior(th, data))
+
+
+@pytest.mark.parametrize('pieces', [1, 2, 3])
+def test_phase_b_pieces_per_lane(data, pieces):
+    """st_tune key 18: 1, 2 or 3 observation pieces per lane in phase B only regroup the per-point
+    sum (pieces, then the wave tree): against scipy within RTOL and against the single-phase kernel
+    within 1e-11, like the default."""
+    from stein_thinning import _native as nat
+    L = nat.lib()
+    assert L.st_tune(18, pieces) == 0
+    try:
+        th = _thetas()
+        got = lv.grad_log_posterior(th, data)
+    finally:
+        L.st_tune(18, -1)
+    want = _single_phase(th, data)
+    err = np.abs(got - want) / np.abs(want).max(axis=1, keepdims=True)
+    assert err.max() < 1e-11, err.max()
+    ref = np.stack([ol.grad_log_posterior(t, data.t, data.y, data.cov) for t in th[:12]])
+    assert (np.abs(got[:12] - ref) / np.abs(ref).max(axis=1, keepdims=True)).max() < RTOL
