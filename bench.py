@@ -642,7 +642,7 @@ def main():
                                    '(run detection + compaction + the thin of the run starts: the drop-in '
                                    'thin\'s default, same indices; "dedup" below); thin_host_arrays = the drop-in '
                                    'thin(sample, gradient, m) on host NumPy arrays (validation, standardisation, '
-                                   'med, H2D, dedup, launch, D2H), timed once after the timed region'},
+                                   'med, H2D, dedup, launch, D2H), the median of three calls after the timed region'},
                        'first_indices': result_idx[:8].tolist()},
             'exchange': exchange,
             'degraded': degraded,
