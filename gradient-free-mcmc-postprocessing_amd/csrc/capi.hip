@@ -614,6 +614,15 @@ int st_layout_soa(const double* rowmajor, int64_t n, int32_t d, int64_t ld, doub
                      "layout launch");
 }
 
+int st_layout_soa_scaled(const double* rowmajor, int64_t n, int32_t d, int64_t ld, const double* scale,
+                         int32_t divide, double* soa, void* stream) {
+    if (!rowmajor || !soa || !scale) return fail(ST_ERR_INVALID, "NULL pointer");
+    if (n < 1 || d < 1 || ld < n) return fail(ST_ERR_INVALID, "bad sizes");
+    return hip_check(st::launch_layout_soa_scaled(rowmajor, n, d, ld, scale, divide ? 1 : 0, soa,
+                                                  static_cast<hipStream_t>(stream)),
+                     "scaled layout launch");
+}
+
 int st_pdist(const double* rows, int64_t k, int32_t d, double* out, void* stream) {
     if (!rows || !out) return fail(ST_ERR_INVALID, "NULL pointer");
     if (k < 2 || k > 65535 || d < 1 || d > st::kMaxDim)

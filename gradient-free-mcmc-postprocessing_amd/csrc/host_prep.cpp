@@ -118,6 +118,17 @@ StatsFn stats_for(int d) {
 
 }  // namespace
 
+namespace st {
+// for st_standardize_upload (prep_upload.cpp): the d = 2 .. 8 single-thread column pass over x
+bool column_stats_fast(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf) {
+    StatsFn f = stats_for(d);
+    if (!f) return false;
+    f(x, n, loc, scl, nan, inf);
+    return true;
+}
+int host_threads() { return hardware_threads(); }
+}  // namespace st
+
 extern "C" int st_standardize_host(const double* sample, const double* gradient, int64_t n,
                                    int32_t d, int32_t standardize, double* sample_out,
                                    double* gradient_out, double* loc_out, double* scl_out,

@@ -597,6 +597,21 @@ __global__ void layout_soa_kernel(const double* __restrict__ rowmajor, int64_t n
     }
 }
 
+// the same with the per-dimension scaling of _validate_and_standardize applied on the way: x / scl
+// (divide) or g * scl -- one IEEE operation per element, the bits of the host's st_standardize_host
+__global__ void layout_soa_scaled_kernel(const double* __restrict__ rowmajor, int64_t n, int d, int64_t ld,
+                                         const double* __restrict__ scale, int divide,
+                                         double* __restrict__ soa) {
+    const int64_t total = n * d;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = e / d;
+        const int k = (int)(e - i * d);
+        const double v = rowmajor[e], c = scale[k];
+        soa[(int64_t)k * ld + i] = divide ? v / c : v * c;
+    }
+}
+
 static int grid_for(int64_t work, int block) {
     int64_t b = (work + block - 1) / block;
     if (b > 2048) b = 2048;
@@ -622,6 +637,12 @@ hipError_t launch_kmat(const PairArgs& p, const int64_t* idx, int64_t k, double*
 hipError_t launch_layout_soa(const double* rowmajor, int64_t n, int d, int64_t ld, double* soa,
                              hipStream_t s) {
     layout_soa_kernel<<<grid_for(n * d, 256), 256, 0, s>>>(rowmajor, n, d, ld, soa);
+    return hipGetLastError();
+}
+
+hipError_t launch_layout_soa_scaled(const double* rowmajor, int64_t n, int d, int64_t ld, const double* scale,
+                                    int divide, double* soa, hipStream_t s) {
+    layout_soa_scaled_kernel<<<grid_for(n * d, 256), 256, 0, s>>>(rowmajor, n, d, ld, scale, divide, soa);
     return hipGetLastError();
 }
 

@@ -1,0 +1,128 @@
+// Host input preparation with the upload running underneath it (the drop-in thin's path, round 4).
+//
+// _validate_and_standardize (JAX_Stein_Thinning.ipynb cells 15-18) needs two sequential passes over
+// the sample's columns -- NumPy's axis-0 reductions are one dependency chain of n adds per column,
+// which bit-exactness keeps on one core (host_prep.cpp) -- and only then can x / scl, g * scl be
+// formed.  st_standardize_host does the scaling on the host and the arrays go up afterwards.  Here
+// thread 0 runs the column passes while the other threads copy the RAW x and g into page-locked
+// staging buffers (with g's NaN / inf scan fused in) and queue each copied chunk's DMA to the device
+// at once, so the upload is finished, or nearly, when the statistics are; the caller then applies
+// the scaling on the device (st_layout_soa_scaled: one IEEE division / multiplication per element,
+// the same bits as the host's).  Returns ST_ERR_UNSUPPORTED outside the d = 2 .. 8, n >= 65536 case
+// the single-thread column pass covers; the caller then takes the st_standardize_host route.
+#include <hip/hip_runtime_api.h>
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#include <algorithm>
+#include <atomic>
+#include <thread>
+#include <vector>
+
+#include <emmintrin.h>
+
+#include "../../include/stein_thinning_hip.h"
+
+namespace st {
+bool column_stats_fast(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf);
+int host_threads();
+}  // namespace st
+
+namespace {
+
+constexpr int64_t kChunk = 1 << 19;   // elements per DMA (4 MB)
+
+// copy src[e0, e1) into stage (16-B aligned base) with non-temporal stores; optionally flag NaN / inf
+void copy_scan(const double* src, double* stage, int64_t e0, int64_t e1, bool scan, bool& nan, bool& inf) {
+    int64_t e = e0;
+    if ((e & 1) && e < e1) {   // to an even element: 16-B aligned stores
+        const double v = src[e];
+        stage[e] = v;
+        nan |= scan && v != v;
+        inf |= scan && fabs(v) == INFINITY;
+        ++e;
+    }
+    const __m128d vinf = _mm_set1_pd(INFINITY);
+    const __m128d absmask = _mm_castsi128_pd(_mm_set1_epi64x(0x7FFFFFFFFFFFFFFFll));
+    __m128d anynan = _mm_setzero_pd(), anyinf = _mm_setzero_pd();
+    for (; e + 1 < e1; e += 2) {
+        const __m128d v = _mm_loadu_pd(src + e);
+        _mm_stream_pd(stage + e, v);
+        if (scan) {
+            anynan = _mm_or_pd(anynan, _mm_cmpunord_pd(v, v));
+            anyinf = _mm_or_pd(anyinf, _mm_cmpeq_pd(_mm_and_pd(v, absmask), vinf));
+        }
+    }
+    nan |= _mm_movemask_pd(anynan) != 0;
+    inf |= _mm_movemask_pd(anyinf) != 0;
+    for (; e < e1; ++e) {
+        const double v = src[e];
+        stage[e] = v;
+        nan |= scan && v != v;
+        inf |= scan && fabs(v) == INFINITY;
+    }
+}
+
+}  // namespace
+
+extern "C" int st_standardize_upload(const double* sample, const double* gradient, int64_t n, int32_t d,
+                                     double* stage_x, double* stage_g, double* dev_x, double* dev_g,
+                                     double* loc_out, double* scl_out, int32_t* status, void* stream) {
+    if (!sample || !gradient || !stage_x || !stage_g || !dev_x || !dev_g || !loc_out || !scl_out || !status)
+        return ST_ERR_INVALID;
+    if ((uintptr_t)stage_x % 16 || (uintptr_t)stage_g % 16) return ST_ERR_INVALID;
+    if (d < 2 || d > 8 || n < 65536) return ST_ERR_UNSUPPORTED;
+    *status = 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    const int64_t total = n * (int64_t)d;
+    const int tc = std::max(1, st::host_threads() - 1);   // copy threads; thread 0 runs the column pass
+    std::vector<char> gnan(tc, 0), ginf(tc, 0);
+    std::atomic<int> dma_err{0};
+    int xnan = 0, xinf = 0;
+    double loc[8], scl[8];
+    std::vector<std::thread> th;
+    th.emplace_back([&] { st::column_stats_fast(sample, n, d, loc, scl, xnan, xinf); });
+    for (int t = 0; t < tc; ++t) {
+        th.emplace_back([&, t] {
+            const int64_t e0 = total * t / tc, e1 = total * (t + 1) / tc;
+            bool nan = false, inf = false;
+            for (int pass = 0; pass < 2; ++pass) {   // this thread's part of x, then of g
+                const double* src = pass ? gradient : sample;
+                double* stage = pass ? stage_g : stage_x;
+                double* dev = pass ? dev_g : dev_x;
+                for (int64_t c = e0; c < e1; c += kChunk) {
+                    const int64_t ce = std::min(c + kChunk, e1);
+                    copy_scan(src, stage, c, ce, pass == 1, nan, inf);
+                    _mm_sfence();   // the staged chunk is in memory before the DMA reads it
+                    if (hipMemcpyAsync(dev + c, stage + c, (size_t)(ce - c) * 8, hipMemcpyHostToDevice, s) !=
+                        hipSuccess)
+                        dma_err.store(1);
+                }
+            }
+            gnan[t] = nan;
+            ginf[t] = inf;
+        });
+    }
+    for (auto& x : th) x.join();
+    if (dma_err.load()) {
+        (void)hipStreamSynchronize(s);
+        return ST_ERR_HIP;
+    }
+    // NaN reported before inf, as the NumPy checks run in that order
+    bool nan = xnan != 0, inf = xinf != 0;
+    for (int t = 0; t < tc; ++t) { nan |= gnan[t] != 0; inf |= ginf[t] != 0; }
+    if (nan || inf) {
+        *status = nan ? 1 : 2;
+    } else {
+        for (int j = 0; j < d; ++j)
+            if (scl[j] == 0.0) *status = 3;
+    }
+    if (*status) {   // the caller drops the buffers: let the queued copies finish reading them first
+        (void)hipStreamSynchronize(s);
+        return ST_OK;
+    }
+    memcpy(loc_out, loc, (size_t)d * 8);
+    memcpy(scl_out, scl, (size_t)d * 8);
+    return ST_OK;
+}

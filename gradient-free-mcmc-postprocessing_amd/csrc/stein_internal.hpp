@@ -155,6 +155,8 @@ hipError_t launch_distance_colsum(const double* a, int64_t lda, int64_t na, cons
                                   double* out, double* ws, int64_t ws_doubles, hipStream_t s);
 hipError_t launch_layout_soa(const double* rowmajor, int64_t n, int d, int64_t ld, double* soa,
                              hipStream_t s);
+hipError_t launch_layout_soa_scaled(const double* rowmajor, int64_t n, int d, int64_t ld, const double* scale,
+                                    int divide, double* soa, hipStream_t s);
 // 'med' preconditioner distances (precon.hip)
 hipError_t launch_pdist(const double* rows, int64_t k, int d, double* out, hipStream_t s);
 // repeated-row compaction (dedup.hip)

@@ -52,6 +52,9 @@ SIGNATURES = {
                                _c_dp]),
     'st_layout_soa': (ctypes.c_int, [_c_dp, _i64, _i32, _i64, _c_dp, _c_dp]),
     'st_pdist': (ctypes.c_int, [_c_dp, _i64, _i32, _c_dp, _c_dp]),
+    'st_layout_soa_scaled': (ctypes.c_int, [_c_dp, _i64, _i32, _i64, _c_dp, _i32, _c_dp, _c_dp]),
+    'st_standardize_upload': (ctypes.c_int, [_c_dp, _c_dp, _i64, _i32, _c_dp, _c_dp, _c_dp, _c_dp,
+                                             _c_dp, _c_dp, _c_dp, _c_dp]),
     'st_run_workspace_bytes': (_i64, [_i64]),
     'st_run_starts': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _c_dp, _c_dp, _i64, _c_dp]),
     'st_run_compact': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _c_dp, _c_dp, _i64, _i64,

@@ -136,6 +136,7 @@ class DeviceProblem:
         if ev is not None:
             ev.synchronize()
             self._upload_event = None
+            self._raw = None
 
     def _soa(self, torch, rowmajor: np.ndarray):
         # page-locked host arrays (thinning._host_buffer) go up asynchronously on the current stream:
@@ -149,6 +150,40 @@ class DeviceProblem:
         nat.check(nat.lib().st_layout_soa(nat.ptr(rm), self.n, self.d, self.ld, nat.ptr(soa),
                                           nat.stream_handle()), 'st_layout_soa')
         return soa
+
+    @classmethod
+    def from_raw_device(cls, x_raw, g_raw, weights: Optional[np.ndarray], scl: np.ndarray,
+                        linv_scale: float, linv_trace: float) -> 'DeviceProblem':
+        """Problem from RAW row-major (n, d) device arrays (thinning._upload_standardized), laid out
+        to SoA with the standardisation applied on the device: x / scl, g * scl (st_layout_soa_scaled).
+        Everything is queued on the current stream without a host wait (small inputs go up from
+        page-locked copies); the upload event marks the end, as for page-locked uploads."""
+        import torch
+        self = cls.__new__(cls)
+        self.device = x_raw.device
+        self.n, self.d = x_raw.shape
+        self.ld = padded_ld(self.n)
+        self.l, self.tr = float(linv_scale), float(linv_trace)
+
+        def up(a):
+            return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64)).pin_memory().to(
+                self.device, non_blocking=True)
+        sc = up(scl)
+        L = nat.lib()
+        self.x = torch.zeros((self.d, self.ld), dtype=torch.float64, device=self.device)
+        self.g = torch.zeros((self.d, self.ld), dtype=torch.float64, device=self.device)
+        for raw, soa, divide in ((x_raw, self.x, 1), (g_raw, self.g, 0)):
+            nat.check(L.st_layout_soa_scaled(nat.ptr(raw), self.n, self.d, self.ld, nat.ptr(sc), divide,
+                                             nat.ptr(soa), nat.stream_handle()), 'st_layout_soa_scaled')
+        self.w = None
+        if weights is not None:
+            self.w = torch.zeros(self.ld, dtype=torch.float64, device=self.device)
+            self.w[:self.n] = up(weights)
+        self._raw = (x_raw, g_raw, sc)   # in use by the queued kernels until the upload event
+        self._async = True
+        self._upload_event = torch.cuda.Event()
+        self._upload_event.record()
+        return self
 
     @classmethod
     def from_soa(cls, x_soa, g_soa, w, n: int, linv_scale: float, linv_trace: float):

@@ -29,9 +29,15 @@ def make_precon(sample: np.ndarray, preconditioner='id', on_device: bool = False
     """
     sample = np.asarray(sample, dtype=np.float64)
     n, d = sample.shape
+    return make_precon_rows(n, d, lambda rows: sample[rows], preconditioner, on_device)
 
+
+def make_precon_rows(n: int, d: int, rows_of, preconditioner='id', on_device: bool = False) -> np.ndarray:
+    """make_precon for an (n, d) sample given only ``rows_of(index array) -> those rows`` of it (the
+    median heuristic reads its subsample rows, nothing else)."""
     def med2():
-        sub = sample[np.linspace(0, n - 1, MED_SUBSAMPLE, dtype=int)] if n > MED_SUBSAMPLE else sample
+        idx = np.linspace(0, n - 1, MED_SUBSAMPLE, dtype=int) if n > MED_SUBSAMPLE else np.arange(n)
+        sub = rows_of(idx)
         if on_device and 2 <= sub.shape[0] <= 65535:
             from .device import pdist_median
             return pdist_median(sub) ** 2

@@ -141,8 +141,10 @@ class SteinIntegrand:
     def __init__(self, sample: np.ndarray, gradient: np.ndarray, linv: np.ndarray,
                  weights: Optional[np.ndarray] = None):
         from .device import isotropic_scale
-        self.sample = sample
-        self.gradient = gradient
+        self._sample = sample
+        self._gradient = gradient
+        self._materialize = None   # deferred host arrays (_deferred): computed on first access
+        self._n = sample.shape[0]
         self.linv = linv
         self.weights = weights
         iso = isotropic_scale(linv)
@@ -154,9 +156,36 @@ class SteinIntegrand:
         self._rows: Optional[np.ndarray] = None
         self._rec = None
 
+    @classmethod
+    def _deferred(cls, n: int, materialize: Callable, linv: np.ndarray,
+                  weights: Optional[np.ndarray] = None) -> 'SteinIntegrand':
+        """Integrand whose standardised host arrays are computed only if something reads them
+        (``materialize() -> (sample, gradient)``): the drop-in thin's device-side standardisation
+        (_upload_standardized) needs them on the host only for the sharded path and host-side
+        helpers."""
+        self = cls(np.empty((n, 0)), np.empty((n, 0)), linv, weights)
+        self._sample = self._gradient = None
+        self._materialize = materialize
+        return self
+
+    def _host_arrays(self) -> None:
+        if self._sample is None:
+            self._sample, self._gradient = self._materialize()
+            self._materialize = None
+
+    @property
+    def sample(self) -> np.ndarray:
+        self._host_arrays()
+        return self._sample
+
+    @property
+    def gradient(self) -> np.ndarray:
+        self._host_arrays()
+        return self._gradient
+
     @property
     def n(self) -> int:
-        return self.sample.shape[0] if self._rows is None else self._rows.shape[0]
+        return self._n if self._rows is None else self._rows.shape[0]
 
     def reindex(self, indices) -> 'SteinIntegrand':
         """View over rows ``indices`` of this integrand (no copy of the device arrays)."""
@@ -246,6 +275,64 @@ def _early_upload(sample: np.ndarray, gradient: np.ndarray, weights: Optional[np
     return DeviceProblem(sample, gradient, weights, 0.0, 0.0)   # l, tr filled in with the preconditioner
 
 
+def _upload_standardized(sample, gradient, standardize: bool):
+    """The drop-in thin's input path when a HIP device is present, d = 2 .. 8 and n >= 65536:
+    st_standardize_upload computes loc / scl on the host while the raw arrays are staged into
+    page-locked buffers and copied to the device underneath, then the device lays them out with the
+    scaling applied (st_layout_soa_scaled: x / scl, g * scl, the host's bits).  Returns
+    (n, d, scl, stage_x, stage_g, x_raw, g_raw) or None (the st_standardize_host route applies).
+    Raises the reference's ValueErrors like _validate_and_standardize."""
+    import ctypes
+    if not standardize:
+        return None
+    try:
+        import torch
+        if not torch.cuda.is_available():
+            return None
+    except Exception:   # noqa: BLE001 -- an optimisation only
+        return None
+    from . import _native as nat
+    sample = np.ascontiguousarray(_as_numpy(sample))
+    gradient = np.ascontiguousarray(_as_numpy(gradient))
+    _validate_shapes(sample, gradient)
+    n, d = sample.shape
+    if not (2 <= d <= 8 and n >= 65536):
+        return None
+    dev = nat.require_device()
+    stage_x, stage_g = _host_buffer(sample.shape), _host_buffer(gradient.shape)
+    if not torch.from_numpy(stage_x).is_pinned():
+        return None
+    x_raw = torch.empty((n, d), dtype=torch.float64, device=dev)
+    g_raw = torch.empty((n, d), dtype=torch.float64, device=dev)
+    loc, scl = np.empty(d), np.empty(d)
+    status = ctypes.c_int32(0)
+    nat.check(nat.lib().st_standardize_upload(
+        sample.ctypes.data, gradient.ctypes.data, n, d, stage_x.ctypes.data, stage_g.ctypes.data,
+        nat.ptr(x_raw), nat.ptr(g_raw), loc.ctypes.data, scl.ctypes.data, ctypes.byref(status),
+        nat.stream_handle()), 'st_standardize_upload')
+    if status.value == 1:
+        raise ValueError('sample or gradient contains NaNs.')
+    if status.value == 2:
+        raise ValueError('sample or gradient contains infs.')
+    if status.value == 3:
+        raise ValueError('Too few unique samples in smp.')
+    return n, d, scl, stage_x, stage_g, x_raw, g_raw
+
+
+def _device_integrand(up, preconditioner, weights: Optional[np.ndarray]) -> SteinIntegrand:
+    """SteinIntegrand over _upload_standardized's device arrays; the host arrays are deferred."""
+    from .device import DeviceProblem
+    from .kernel import make_precon_rows
+    n, d, scl, stage_x, stage_g, x_raw, g_raw = up
+    prob = DeviceProblem.from_raw_device(x_raw, g_raw, weights, scl, 0.0, 0.0)
+    # the preconditioner's subsample rows, standardised on the host (x / scl: the same IEEE divisions)
+    linv = make_precon_rows(n, d, lambda rows: stage_x[rows] / scl, preconditioner, on_device=True)
+
+    def materialize():
+        return _validate_and_standardize(stage_x, stage_g, True)
+    return _attach(SteinIntegrand._deferred(n, materialize, linv, weights), prob)
+
+
 def _attach(integrand: SteinIntegrand, prob) -> SteinIntegrand:
     if prob is not None:
         prob.l, prob.tr = float(integrand.linv_scale), float(integrand.linv_trace)
@@ -257,6 +344,9 @@ def _attach(integrand: SteinIntegrand, prob) -> SteinIntegrand:
 
 
 def _make_stein_integrand(sample, gradient, standardize: bool = True, preconditioner='id') -> SteinIntegrand:
+    up = _upload_standardized(sample, gradient, standardize)
+    if up is not None:
+        return _device_integrand(up, preconditioner, None)
     sample, gradient = _validate_and_standardize(sample, gradient, standardize)
     prob = _early_upload(sample, gradient, None) if preconditioner == 'med' else None
     linv = make_precon(sample, preconditioner, on_device=prob is not None)
@@ -265,15 +355,21 @@ def _make_stein_integrand(sample, gradient, standardize: bool = True, preconditi
 
 def _make_stein_gf_integrand(sample, log_p, log_q, gradient_q, standardize: bool = True,
                              range_cap: Optional[float] = None, preconditioner='id') -> SteinIntegrand:
-    sample, gradient_q = _validate_and_standardize(sample, gradient_q, standardize)
+    up = _upload_standardized(sample, gradient_q, standardize)
+    if up is None:
+        sample, gradient_q = _validate_and_standardize(sample, gradient_q, standardize)
+        n = sample.shape[0]
+    else:
+        n = up[0]
     log_p = _as_numpy(log_p).reshape(-1)
     log_q = _as_numpy(log_q).reshape(-1)
-    n = sample.shape[0]
     if log_p.shape[0] != n or log_q.shape[0] != n:
         raise ValueError('Dimensions of sample and log densities are inconsistent.')
     if np.isnan(log_p).any() or np.isnan(log_q).any():
         raise ValueError('log_p or log_q contains NaNs.')
     weights = np.exp(_log_weights(log_p, log_q, range_cap))
+    if up is not None:
+        return _device_integrand(up, preconditioner, weights)
     prob = _early_upload(sample, gradient_q, weights) if preconditioner == 'med' else None
     linv = make_precon(sample, preconditioner, on_device=prob is not None)
     return _attach(SteinIntegrand(sample, gradient_q, linv, weights), prob)

@@ -363,9 +363,24 @@ int st_run_compact(const double *x_soa, const double *g_soa, const double *weigh
                    int64_t ld, const uint8_t *starts, const void *workspace, int64_t count, int64_t ld_out,
                    double *x_out, double *g_out, double *w_out, int32_t *rows_out, void *stream);
 
+/* The same with the upload underneath: thread 0 computes loc / scl (st_standardize_host's column
+ * passes, bit-identical) while the other threads copy the RAW arrays into the page-locked staging
+ * buffers stage_x / stage_g (16-B aligned, n d doubles; g's NaN / inf scan fused in) and queue each
+ * copied chunk's host-to-device copy into dev_x / dev_g (row-major) on `stream`.  The caller scales
+ * on the device (st_layout_soa_scaled with loc_out / scl_out).  d = 2 .. 8 and n >= 65536 only
+ * (ST_ERR_UNSUPPORTED otherwise: use st_standardize_host); *status as st_standardize_host's (on a
+ * nonzero status the queued copies have finished when it returns). */
+int st_standardize_upload(const double *sample, const double *gradient, int64_t n, int32_t d,
+                          double *stage_x, double *stage_g, double *dev_x, double *dev_g,
+                          double *loc_out, double *scl_out, int32_t *status, void *stream);
+
 /* row-major (n, d) -> SoA (d, ld) layout helper (device to device) */
 int st_layout_soa(const double *rowmajor, int64_t n, int32_t d, int64_t ld, double *soa,
                   void *stream);
+/* the same with x / scale[k] (divide = 1) or x * scale[k] (divide = 0) per element: the scaling of
+ * _validate_and_standardize on the device (scale: d doubles in device memory) */
+int st_layout_soa_scaled(const double *rowmajor, int64_t n, int32_t d, int64_t ld, const double *scale,
+                         int32_t divide, double *soa, void *stream);
 
 #ifdef __cplusplus
 }
