@@ -194,6 +194,7 @@ struct PersistArgs {
     int RL;               // LDS-resident rows per block
     int stream_a_lds;     // 512-thread kernels: the streamed rows' running sums are kept in LDS
     int poll_delay;       // s_memrealtime ticks added before aligning a step's first poll (st_tune key 16)
+    int lds_two_chains;   // 512-thread kernels: two LDS chunks as two independent chains (st_tune key 19)
     uint64_t* stamps;     // diagnostic build only (ST_PERSIST_STAMPS): [G][kStampSteps][kStampPhases]
     int rec_stride;               // record pitch in granules (2 = packed; wider spreads the polled
                                   // records over more memory channels)
@@ -988,7 +989,36 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
                             take_stream(s1, av1);
                         } else if (c >= nS && c + 1 < nC) {   // two LDS chunks: two chains
                             const int e0 = ((c - nS) << 6) + lane, e1 = e0 + 64;
-                            const double av0 = lds_pair(e0), av1 = lds_pair(e1);
+                            double av0, av1;
+                            if (a.lds_two_chains) {
+                                // both rows' fields (running sums included) read up front, then two
+                                // independent chains with no LDS access between them, then both
+                                // stores: the scheduler can interleave the chains (lds_pair's store
+                                // of the first row's sum kept the second row's reads behind it)
+                                double* const rp0 = lrow(e0);
+                                double* const rp1 = lrow(e1);
+                                SRow ra, rb;
+#pragma unroll
+                                for (int k = 0; k < D; ++k) {
+                                    ra.x[k] = rp0[fX + k * 64]; ra.g[k] = rp0[fG + k * 64];
+                                    rb.x[k] = rp1[fX + k * 64]; rb.g[k] = rp1[fG + k * 64];
+                                }
+                                ra.a = rp0[fA];
+                                rb.a = rp1[fA];
+                                ra.w = GF ? rp0[fW] : 1.0;
+                                rb.w = GF ? rp1[fW] : 1.0;
+                                av0 = stream_pair(ra);
+                                av1 = stream_pair(rb);
+                                if constexpr (!FAST) {
+                                    av0 = lds_base + e0 < r1 ? av0 : INFINITY;
+                                    av1 = lds_base + e1 < r1 ? av1 : INFINITY;
+                                }
+                                rp0[fA] = av0;
+                                rp1[fA] = av1;
+                            } else {
+                                av0 = lds_pair(e0);
+                                av1 = lds_pair(e1);
+                            }
                             scan_take_idx<FAST>(av0, (uint32_t)(lds_base + e0), bv, bi);
                             scan_take_idx<FAST>(av1, (uint32_t)(lds_base + e1), bv, bi);
                         } else {                     // the stream/LDS seam or the last chunk
@@ -1134,6 +1164,14 @@ static int g_persist_sal = 0;
 // 6.86, 20 and 25 slower; n = 1e6 and 4e5 (general 512-thread kernel) and 2e5 / 2.5e5 (256-thread
 // kernels): every delay slower or equal.
 static int g_persist_delay = -1;
+// st_tune key 19: 512-thread kernels, two LDS chunks as two independent dependency chains (fields read
+// up front, sums stored after both) -- 1 / -1 automatic; 0 = one lds_pair after the other (round 4's
+// earlier form, whose LDS store of the first sum held the second row's reads and chain behind it).
+// Same box, alternating (profiles/r04_lds_two_chains.log): config 4 6.91-6.94 (0) -> 6.80-6.81 (1) ms
+// per thin.  The two pair evaluations interleaved statement by statement in the source as well were
+// measured and dropped: the extra live registers spilled inside the step loop (75 VGPRs of scratch)
+// and every variant ran at 8.6-8.7 ms (profiles/r04_lds_interleaved_rejected.log)
+static int g_persist_lds2 = -1;
 // automatic register rows of the compact-only kernel: 9 (28 B of scratch at d = 4) unless more than
 // kCmpStreamRows rows per block would still be streamed, then 10 (108 B of scratch; the streamed
 // rows then no longer stay in the XCD's L2).  Same-box, d = 4, m = 1000 (profiles/r03_compact_only_rt.log):
@@ -1188,6 +1226,11 @@ int persistent_tune(int key, int value) {
     if (key == 15) {
         if (value < -1 || value > 1) return -1;
         g_persist_sal = value < 0 ? 0 : value;
+        return 0;
+    }
+    if (key == 19) {
+        if (value < -1 || value > 1) return -1;
+        g_persist_lds2 = value;
         return 0;
     }
     return -1;
@@ -1373,6 +1416,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     a.RL = (int)RL;
     a.stream_a_lds = sal;
     a.poll_delay = g_persist_delay >= 0 ? g_persist_delay : 0;
+    a.lds_two_chains = g_persist_lds2 >= 0 ? g_persist_lds2 : 1;
     a.rec_stride = pitch;
     a.nrep = nrep;
     a.rep_stride = persistent_rep_stride(G, pitch, nrep);

@@ -87,7 +87,9 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * timing only, same results), key 17 = LV gradient phase B: 1 reads the observation times / data
  * from global memory as round 3 did (0 / -1 = automatic: staged in LDS when 3 t_n doubles fit
  * 64 KB; same results), key 18 = LV gradient phase B: observation pieces per lane (1, 2, 3; -1 =
- * automatic; the per-point sum is reassociated differently, within the 1e-8 tolerance).
+ * automatic; the per-point sum is reassociated differently, within the 1e-8 tolerance), key 19 =
+ * 512-thread persistent kernels: two LDS-row chunks computed as two independent chains (1 / -1 =
+ * automatic) or one after the other (0; same results).
  */
 int st_tune(int32_t key, int32_t value);
 

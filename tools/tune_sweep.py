@@ -34,7 +34,7 @@ m = cfg['m']
 L = nat.lib()
 ref = None
 for st in settings:
-    for k in (3, 4, 5, 8, 9, 10, 15, 16):
+    for k in (3, 4, 5, 8, 9, 10, 15, 16, 19):
         L.st_tune(k, -1)
     for kv in st.split(','):
         k, v = (int(x) for x in kv.split('='))
