@@ -679,7 +679,8 @@ def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None
     if world > 1 and not _group_same(np.array([-1 if rows is None else rows.size], dtype=np.int64), group):
         raise ValueError('sharded thin: the ranks disagree on the repeated-row path '
                          '(stein_thinning.set_dedup / ST_DEDUP must agree, and so must the sample)')
-    global last_mode
+    global last_mode, last_rows_kept
+    last_rows_kept = None if rows is None else int(rows.size)
     runner = sharded_runner(integrand, n_points, group, use_graph)
     last_mode = runner.mode
     idx = runner.indices()
@@ -687,3 +688,4 @@ def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None
 
 
 last_mode = None   # exchange engine of the last sharded thin in this process (tests / bench)
+last_rows_kept = None   # rows the last sharded thin kept after dropping repeats (None: all)

@@ -149,6 +149,46 @@ def _dropin_worker(rank, world, port, out_dir):
         dist.destroy_process_group()
 
 
+def _chain_data(n=60_001, d=4):
+    """Random-walk chain with ~70 % of its rows repeating the row before (the repeated-row path)."""
+    rng = np.random.default_rng(17)
+    x = np.empty((n, d))
+    x[0] = rng.normal(size=d)
+    acc = rng.random(n) < 0.3
+    for i in range(1, n):
+        x[i] = x[i - 1] + 0.3 * rng.normal(size=d) if acc[i] else x[i - 1]
+    return x, -x * np.linspace(0.5, 2.0, d)
+
+
+def _dropin_dedup_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port), ST_SHARDED_EXCHANGE='device',
+                      ST_SHARD_THIN='1')
+    torch.cuda.set_device(0)
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from stein_thinning import distributed as sd
+        from stein_thinning import thinning as st
+        x, g = _chain_data()
+        idx = st.thin(x, g, 60, preconditioner='med')
+        np.save(os.path.join(out_dir, f'didx{rank}.npy'), idx)
+        with open(os.path.join(out_dir, f'dkept{rank}.txt'), 'w') as f:
+            f.write(str(sd.last_rows_kept))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_dropin_sharded_thin_drops_repeated_rows(tmp_path):
+    """The row-sharded drop-in thin compacts a chain's repeated rows on the host before sharding
+    (SteinIntegrand.run_starts_view): every rank returns the NumPy path's indices."""
+    mp.spawn(_dropin_dedup_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
+    x, g = _chain_data()
+    want = o.thin(x, g, 60, preconditioner='med')
+    for r in range(2):
+        kept = int((tmp_path / f'dkept{r}.txt').read_text())
+        assert 0 < kept < 0.5 * x.shape[0]
+        np.testing.assert_array_equal(np.load(tmp_path / f'didx{r}.npy'), want)
+
+
 def test_dropin_thin_shards_across_two_processes(tmp_path):
     mp.spawn(_dropin_worker, args=(2, _free_port(), str(tmp_path)), nprocs=2, join=True)
     for run, gf in enumerate([False, True]):
