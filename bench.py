@@ -634,7 +634,7 @@ def main():
                        'wallclock_thin_s': {
                            'device_resident': elapsed / args.steps,
                            'device_resident_dedup': (round(dedup['s_per_thin_incl_detect'], 6)
-                                                     if rank == 0 and dedup else None),
+                                                     if rank == 0 and dedup and dedup.get('used') else None),
                            'thin_host_arrays': e2e['thin_host_arrays_s'] if rank == 0 and e2e else None,
                            'note': 'device_resident = ms_per_step: the timed thin of the standardised sample '
                                    'already in HBM, every one of the n m pairs evaluated (value); '
