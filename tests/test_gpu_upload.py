@@ -94,3 +94,19 @@ def test_device_standardisation_errors():
             st._make_stein_integrand(a, b, preconditioner='med')
         with pytest.raises(ValueError, match=msg):
             st._validate_and_standardize(a, b, True)
+
+
+def test_device_standardisation_input_kinds():
+    """The device route takes what _validate_and_standardize takes: float32 arrays, Fortran-ordered
+    arrays and torch tensors (CPU or on the GPU) give the float64 NumPy route's indices."""
+    n = 70_001
+    x, g = _data(n=n, seed=11)
+    want = st.thin(x, g, 15, preconditioner='med')
+    np.testing.assert_array_equal(want, o.thin(x, g, 15, preconditioner='med'))
+    x32, g32 = x.astype(np.float32), g.astype(np.float32)
+    np.testing.assert_array_equal(st.thin(x32, g32, 15, preconditioner='med'),
+                                  o.thin(x32.astype(np.float64), g32.astype(np.float64), 15, preconditioner='med'))
+    np.testing.assert_array_equal(st.thin(np.asfortranarray(x), np.asfortranarray(g), 15, preconditioner='med'), want)
+    np.testing.assert_array_equal(st.thin(torch.from_numpy(x), torch.from_numpy(g), 15, preconditioner='med'), want)
+    np.testing.assert_array_equal(st.thin(torch.from_numpy(x).cuda(), torch.from_numpy(g).cuda(), 15,
+                                          preconditioner='med'), want)
