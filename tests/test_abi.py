@@ -102,6 +102,26 @@ def test_host_side_validation_of_the_newer_entry_points(libpath):
     # host standardisation: bad arguments
     status = ctypes.c_int32(0)
     assert lib.st_standardize_host(None, None, 10, 4, 1, None, None, None, None, ctypes.byref(status)) == inv
+    # standardisation with the upload underneath: NULLs, unaligned staging, and the cases it leaves to
+    # st_standardize_host (d outside 2 .. 8, n < 65536) -- all before any HIP call
+    st = [p, p, 100_000, 4, p, p, p, p, p, p, ctypes.byref(status), None]
+    assert lib.st_standardize_upload(None, *st[1:]) == inv
+    odd = ctypes.c_void_p(p.value + 8)
+    assert lib.st_standardize_upload(*(st[:4] + [odd] + st[5:])) == inv
+    assert lib.st_standardize_upload(*(st[:3] + [9] + st[4:])) == _native.ST_ERR_UNSUPPORTED
+    assert lib.st_standardize_upload(*(st[:2] + [1000] + st[3:])) == _native.ST_ERR_UNSUPPORTED
+    # repeated-row compaction, scaled layout, 'med' distances
+    assert lib.st_run_workspace_bytes(1) > 0 and lib.st_run_workspace_bytes(1 << 20) >= 8 + 8 * 1024
+    assert lib.st_run_starts(p, p, None, 10, 4, 16, None, p, 1 << 10, None) == inv          # no output
+    assert lib.st_run_starts(p, p, None, 10, 4, 16, p, p, 8, None) == inv                   # workspace too small
+    assert lib.st_run_starts(p, p, None, 10, 4, 12, p, p, 1 << 10, None) == inv             # ld % 8
+    assert lib.st_run_compact(p, p, None, 10, 4, 16, p, p, 11, 16, p, p, None, p, None) == inv   # count > n
+    assert lib.st_run_compact(p, p, None, 10, 4, 16, p, p, 5, 4, p, p, None, p, None) == inv     # ld_out < count
+    assert lib.st_run_compact(p, p, p, 10, 4, 16, p, p, 5, 8, p, p, None, p, None) == inv        # weights, no w_out
+    assert lib.st_layout_soa_scaled(p, 10, 4, 8, p, 1, p, None) == inv                     # ld < n
+    assert lib.st_layout_soa_scaled(p, 10, 4, 16, None, 1, p, None) == inv                 # no scale
+    assert lib.st_pdist(p, 1, 4, p, None) == inv and lib.st_pdist(p, 70_000, 4, p, None) == inv
+    assert lib.st_pdist(p, 10, 0, p, None) == inv and lib.st_pdist(None, 10, 4, p, None) == inv
 
 
 def test_library_is_gfx950_only(libpath):
@@ -118,7 +138,8 @@ def test_tune_keys_validate_without_gpu(libpath):
     lib = _native.load_library(libpath)
     for key, good, bad in [(10, [1, 2, 16, 32], [0, 3, 64]), (9, [16, 256, 4096], [8, 24, 8192]),
                            (4, [256, 512], [128, 1024]), (8, [1, 2], [3]), (11, [0, 1], [2, -2]),
-                           (12, [0, 8, 9, 10], [7, 11]), (13, [0, 1, 2, 5, 6], [7, -2])]:
+                           (12, [0, 8, 9, 10], [7, 11]), (13, [0, 1, 2, 5, 6], [7, -2]),
+                           (17, [0, 1], [2, -2]), (18, [1, 2, 3], [0, 4]), (19, [0, 1], [2, -2])]:
         for v in good:
             assert lib.st_tune(key, v) == 0, (key, v)
         for v in bad:
