@@ -27,6 +27,15 @@ int hip_check(hipError_t e, const char* what) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+}  // namespace
+
+namespace st {
+// st_last_error text for entry points defined in other translation units (prep_upload.cpp)
+int report_error(int code, const char* msg) { return fail(code, "%s", msg); }
+}  // namespace st
+
+namespace {
+
 int check_problem(const double* x, const double* g, const double* w, int64_t n, int32_t d,
                   int64_t ld) {
     if (!x || !g) return fail(ST_ERR_INVALID, "sample/gradient pointer is NULL");

@@ -27,6 +27,7 @@
 namespace st {
 bool column_stats_fast(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf);
 int host_threads();
+int report_error(int code, const char* msg);   // capi.hip: sets st_last_error()
 }  // namespace st
 
 namespace {
@@ -70,9 +71,11 @@ extern "C" int st_standardize_upload(const double* sample, const double* gradien
                                      double* stage_x, double* stage_g, double* dev_x, double* dev_g,
                                      double* loc_out, double* scl_out, int32_t* status, void* stream) {
     if (!sample || !gradient || !stage_x || !stage_g || !dev_x || !dev_g || !loc_out || !scl_out || !status)
-        return ST_ERR_INVALID;
-    if ((uintptr_t)stage_x % 16 || (uintptr_t)stage_g % 16) return ST_ERR_INVALID;
-    if (d < 2 || d > 8 || n < 65536) return ST_ERR_UNSUPPORTED;
+        return st::report_error(ST_ERR_INVALID, "st_standardize_upload: NULL pointer");
+    if ((uintptr_t)stage_x % 16 || (uintptr_t)stage_g % 16)
+        return st::report_error(ST_ERR_INVALID, "st_standardize_upload: staging buffers must be 16-byte aligned");
+    if (d < 2 || d > 8 || n < 65536)
+        return st::report_error(ST_ERR_UNSUPPORTED, "st_standardize_upload: d = 2 .. 8 and n >= 65536 only");
     *status = 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
     const int64_t total = n * (int64_t)d;
@@ -107,7 +110,7 @@ extern "C" int st_standardize_upload(const double* sample, const double* gradien
     for (auto& x : th) x.join();
     if (dma_err.load()) {
         (void)hipStreamSynchronize(s);
-        return ST_ERR_HIP;
+        return st::report_error(ST_ERR_HIP, "st_standardize_upload: a host-to-device copy could not be queued");
     }
     // NaN reported before inf, as the NumPy checks run in that order
     bool nan = xnan != 0, inf = xinf != 0;

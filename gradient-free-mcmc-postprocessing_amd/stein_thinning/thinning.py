@@ -325,12 +325,17 @@ def _device_integrand(up, preconditioner, weights: Optional[np.ndarray]) -> Stei
     from .kernel import make_precon_rows
     n, d, scl, stage_x, stage_g, x_raw, g_raw = up
     prob = DeviceProblem.from_raw_device(x_raw, g_raw, weights, scl, 0.0, 0.0)
-    # the preconditioner's subsample rows, standardised on the host (x / scl: the same IEEE divisions)
-    linv = make_precon_rows(n, d, lambda rows: stage_x[rows] / scl, preconditioner, on_device=True)
 
     def materialize():
         return _validate_and_standardize(stage_x, stage_g, True)
-    return _attach(SteinIntegrand._deferred(n, materialize, linv, weights), prob)
+    try:
+        # the preconditioner's subsample rows, standardised on the host (x / scl: the same IEEE divisions)
+        linv = make_precon_rows(n, d, lambda rows: stage_x[rows] / scl, preconditioner, on_device=True)
+        integrand = SteinIntegrand._deferred(n, materialize, linv, weights)
+    except Exception:
+        prob.wait_upload()   # the queued copies read the staging buffers about to be dropped
+        raise
+    return _attach(integrand, prob)
 
 
 def _attach(integrand: SteinIntegrand, prob) -> SteinIntegrand:
