@@ -136,3 +136,33 @@ def test_thin_default_and_switch(monkeypatch):
     log_q = -0.6 * np.sum(x * x, axis=1)
     np.testing.assert_array_equal(st.thin_gf(x, log_p, log_q, -1.2 * x, 30, preconditioner='med'),
                                   o.thin_gf(x, log_p, log_q, -1.2 * x, 30, preconditioner='med'))
+
+
+@pytest.mark.parametrize('gf', [False, True])
+def test_dedup_bit_exact_outside_fast_range(gf):
+    """Rows outside [2^-60, 2^60] (whole runs of them, and run starts whose repeats follow) take the
+    general arithmetic's per-pair rule -- still a function of the two rows only, so the thin of the run
+    starts matches the full thin and the C bit model bit for bit."""
+    n, m = 120_001, 40
+    x, g = _chain(n, 4, seed=31)
+    s, gs, w, l, tr = _inputs(x, g, gf)
+    starts = np.flatnonzero(np.r_[True, np.any(s[1:] != s[:-1], axis=1)])
+    rng = np.random.default_rng(5)
+    pick = rng.choice(starts[:-1], size=10, replace=False)
+    for k, r in enumerate(pick):          # modify whole runs so they stay runs
+        end = starts[np.searchsorted(starts, r) + 1]
+        if k < 4:
+            gs[r:end, 0] = 1e-25
+        elif k < 7:
+            gs[r:end, -1] = 2e19
+        else:
+            s[r:end, 1] = 1e-30
+    prob = DeviceProblem(s, gs, w, l, tr)
+    assert prob.dedup_view() is not None
+    want, want_A = prob.greedy(m, return_sums=True)
+    got, got_A = prob.greedy(m, return_sums=True, dedup='always')
+    np.testing.assert_array_equal(got, want)
+    assert np.array_equal(got_A, want_A)
+    cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
+    np.testing.assert_array_equal(got, cidx)
+    assert np.array_equal(got_A, cA)
