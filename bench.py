@@ -387,7 +387,10 @@ def main():
                     help='energy kernel work units per launch (st_tune key 14; -1 = auto)')
     ap.add_argument('--arith', default='compact', choices=['compact', 'exact'],
                     help='arithmetic of the d <= 8 greedy kernels (stein_thinning.set_arithmetic)')
-    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks'],
+    ap.add_argument('--chains', type=int, default=8, help='chains workload: independent chains thinned')
+    ap.add_argument('--in-flight', type=int, default=-1,
+                    help='chains workload: thins in flight at once (-1 = stein_thinning.device.IN_FLIGHT)')
+    ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks', 'chains'],
                     help='thin: the headline greedy thin (default); ksd: full-sample cumulative KSD '
                          '(row-sharded, RCCL all-reduce of the n-length column-sum vector); ranks: launcher '
                          'check only (gloo, no GPU)')
@@ -410,6 +413,8 @@ def main():
         return main_proxy(args)
     if args.workload == 'lv':
         return main_lv(args)
+    if args.workload == 'chains':
+        return main_chains(args)
 
     import torch
     import torch.distributed as dist
@@ -661,6 +666,71 @@ def thinned_sizes(n_points_calculate: int = 1000) -> np.ndarray:
     """Comparison.ipynb cell 21: 50 sizes on [5, 100] and 200 on [100, n_points_calculate]."""
     return np.concatenate([np.linspace(5, 100, 50).astype(int),
                            np.linspace(100, n_points_calculate, 200).astype(int)])
+
+
+def main_chains(args):
+    """The reference's per-chain LV thinning (Stein_thinning.ipynb cell 12: every RW-MH chain of
+    n ~ 5e5 thinned on its own to m = 10 000 with 'med'; the fan-out is code/src/utils/parallel.py:48-52)
+    for `--chains` seeded surrogate chains (lv_call_shape 'exp'), standardised arrays resident on the
+    GPU.  A step = all the chains' thins: one after the other (the loop the notebook runs) and side by
+    side (stein_thinning.device.greedy_concurrent, each latency-bound thin on a share of the CUs);
+    both drop repeated rows first (the drop-in thin's default), and the indices must agree.  `value`
+    = chains thinned per second by greedy_concurrent; N > 1: the chains are dealt to the ranks."""
+    import torch
+    import torch.distributed as dist
+    from stein_thinning import device as sdev
+    from stein_thinning import thinning as st
+    rank, world, dev = _setup_ranks()
+    if world > 1:
+        _init_group(dev)
+    n, m = 500_000, 10_000
+    mine = list(range(rank, args.chains, world))
+    probs = [st._make_stein_integrand(*lv_call_shape(n, 20_000 + k, 'exp'), preconditioner='med').device_problem()
+             for k in mine]
+    in_flight = args.in_flight if args.in_flight > 0 else sdev.IN_FLIGHT
+
+    def run(c):
+        for p in probs:
+            p._dedup = False   # run detection inside the timed region
+        return sdev.greedy_concurrent(probs, m, in_flight=c)
+    seq = run(1)
+    for _ in range(args.warmup):
+        run(in_flight)
+    times, seq_times = [], []
+    for _ in range(args.steps):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        got = run(in_flight)
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+    for _ in range(2):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        run(1)
+        torch.cuda.synchronize()
+        seq_times.append(time.perf_counter() - t0)
+    same = all(np.array_equal(a, b) for a, b in zip(got, seq))
+    elapsed = float(np.median(times))
+    if world > 1:
+        elapsed = _max_over_ranks([elapsed], dev)[0]
+    if rank == 0:
+        line = {'metric': 'independent chain thins per second (the reference LV call shape: n=5e5, m=1e4 per chain)',
+                'value': args.chains / elapsed, 'unit': 'chains/s', 'n_gpus': world, 'steps': args.steps,
+                'warmup': args.warmup, 'ms_per_step': elapsed * 1e3, 'higher_is_better': True, 'scaling': 'strong',
+                'vs_baseline': None, 'dtype': 'f64',
+                'data': 'synthetic (seeded RW-MH LV-surrogate chains, one per seed; see bench.py lv_call_shape)',
+                'config': {'workload': f"{args.chains} chains x thin(np.exp(s), grads, 10_000, 'med')",
+                           'n_per_chain': n, 'm': m, 'in_flight': in_flight,
+                           'run_starts': [p.dedup_view().n_unique if p.dedup_view() is not None else p.n for p in probs],
+                           'parallelism': f'chains dealt to {world} ranks' if world > 1 else 'single-gpu'},
+                'one_after_the_other_ms': round(float(np.median(seq_times)) * 1e3, 2),
+                'side_by_side_ms': round(elapsed * 1e3, 2),
+                'same_indices_as_one_after_the_other': bool(same)}
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main_energy(args):

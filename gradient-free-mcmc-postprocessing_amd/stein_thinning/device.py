@@ -369,3 +369,64 @@ class DeviceProblem:
             nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), k, self.ld, self.d, self.l, self.tr,
             nat.ptr(out), nat.stream_handle()), 'st_kmat')
         return out.cpu().numpy()
+
+
+# thins in flight at once in greedy_concurrent: 8 chains of the reference's LV call shape (5e5 rows,
+# m = 10 000, repeated rows dropped, run detection included) took 83 ms with 4 in flight (64-block
+# grids) and 156 ms with 2, against 258-264 ms one after the other (profiles/r04_chains_probe.log)
+IN_FLIGHT = 4
+
+
+def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, dedup=True) -> list:
+    """Independent greedy thins on ONE GPU at the same time (the reference thins every MCMC chain on
+    its own: Stein_thinning.ipynb, fan-out code/src/utils/parallel.py:48-52).  Each problem's launch
+    runs on one of ``in_flight`` streams with a grid of #CU / in_flight blocks (st_tune key 5, restored
+    afterwards), so that many latency-bound thins share the chip instead of queueing behind each
+    other.  Every result equals
+    ``problem.greedy(n_points, dedup=dedup)``; a launch whose bounded waits expired anyway (another
+    process's kernels held CUs) is re-run alone.  Returns one uint32 index array per problem."""
+    import torch
+    problems = list(problems)
+    if not problems:
+        return []
+    L = nat.lib()
+    k = len(problems)
+    c = max(1, min(k, in_flight if in_flight is not None else IN_FLIGHT))
+    if c == 1:   # one at a time, full grid
+        return [p.greedy(n_points, dedup=dedup) for p in problems]
+    cus = torch.cuda.get_device_properties(problems[0].device).multi_processor_count
+    views = []
+    for p in problems:
+        v = None
+        if dedup == 'always' or (dedup and p.dedup_pays(n_points)):
+            v = p.dedup_view()
+            if v is not None and dedup != 'always' and not p.dedup_pays(n_points, v.n_unique):
+                v = None
+        views.append(v)
+    runs = [v.problem if v is not None else p for p, v in zip(problems, views)]
+    # c streams, problem i on stream i % c: at most c grids of #CU / c blocks are ever resident
+    # together, so every grid fits beside the others
+    cur = torch.cuda.current_stream()
+    pool = [torch.cuda.Stream(device=runs[0].device) for _ in range(c)]
+    for s in pool:
+        s.wait_stream(cur)   # the problems' arrays were written on the current stream
+    bufs, streams = [], []
+    nat.check(L.st_tune(5, max(1, cus // c)), 'st_tune')
+    try:
+        for i, p in enumerate(runs):
+            s = pool[i % c]
+            with torch.cuda.stream(s):
+                b = p.greedy_buffers(n_points)
+                p.greedy_launch(n_points, *b)
+            bufs.append(b)
+            streams.append(s)
+    finally:
+        L.st_tune(5, -1)
+    out = []
+    for p, v, b, s in zip(runs, views, bufs, streams):
+        s.synchronize()
+        idx = b[0].cpu().numpy().view(np.uint32).copy()
+        if idx.size and int(idx.max()) >= p.n:   # not co-resident next to the others: alone now
+            idx, _ = p._greedy_run(n_points)
+        out.append(v.to_rows(idx) if v is not None else idx)
+    return out

@@ -466,6 +466,21 @@ def thin(sample, gradient, n_points: int, standardize: bool = True, precondition
     return _greedy_search(n_points, integrand)
 
 
+def thin_chains(samples, gradients, n_points: int, standardize: bool = True, preconditioner='id') -> list:
+    """``[thin(s, g, n_points, standardize, preconditioner) for s, g in zip(samples, gradients)]``
+    -- the reference's per-chain loop (Stein_thinning.ipynb) -- with the thins running side by side
+    on one GPU (device.greedy_concurrent: each latency-bound thin on a share of the CUs); the same
+    indices as the loop."""
+    from .device import greedy_concurrent
+    integrands = [_make_stein_integrand(s, g, standardize, preconditioner) for s, g in zip(samples, gradients)]
+    n_points = int(n_points)
+    if n_points < 0:
+        raise ValueError('negative dimensions are not allowed')
+    if n_points == 0:
+        raise IndexError('index 0 is out of bounds for axis 0 with size 0')
+    return greedy_concurrent([i.device_problem() for i in integrands], n_points, dedup=_dedup())
+
+
 def thin_gf(sample, log_p, log_q, gradient_q, n_points: int, standardize: bool = True,
             range_cap: Optional[float] = None, preconditioner='id') -> np.ndarray:
     """Gradient-free Stein thinning with auxiliary density q (report.tex:390-426)."""

@@ -166,3 +166,23 @@ def test_dedup_bit_exact_outside_fast_range(gf):
     cidx, cA = oracle_c.greedy(s, gs, w, l, tr, m)
     np.testing.assert_array_equal(got, cidx)
     assert np.array_equal(got_A, cA)
+
+
+@pytest.mark.parametrize('dedup', [True, False])
+def test_thin_chains_equal_the_per_chain_loop(dedup, monkeypatch):
+    """stein_thinning.thin_chains (device.greedy_concurrent: the chains' persistent launches side by
+    side, each on a share of the CUs) returns the reference loop's indices for every chain."""
+    from stein_thinning import device
+    monkeypatch.setattr(device, 'DEDUP_MIN_SAVING_S', 0.0)   # take the repeated-row path at this size
+    chains = [_chain(70_000 + 1_000 * k, 4, seed=50 + k) for k in range(6)]
+    stein_thinning.set_dedup(dedup)
+    try:
+        got = stein_thinning.thin_chains([c[0] for c in chains], [c[1] for c in chains], 40,
+                                         preconditioner='med')
+        want = [st.thin(x, g, 40, preconditioner='med') for x, g in chains]
+    finally:
+        stein_thinning.set_dedup(None)
+    assert len(got) == len(chains)
+    for a, b in zip(got, want):
+        np.testing.assert_array_equal(a, b)
+    np.testing.assert_array_equal(want[0], o.thin(chains[0][0], chains[0][1], 40, preconditioner='med'))
