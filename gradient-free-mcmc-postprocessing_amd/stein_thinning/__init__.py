@@ -7,6 +7,6 @@ _make_stein_integrand, _make_stein_gf_integrand}``, ``stein_thinning.stein.{ksd,
 RCCL): ``stein_thinning.distributed``.  Importing this package touches no GPU.
 """
 from ._native import set_arithmetic  # noqa: F401
-from .thinning import set_dedup, set_rank_sharding, thin, thin_chains, thin_gf  # noqa: F401
+from .thinning import set_dedup, set_rank_sharding, thin, thin_chains, thin_gf, thin_gf_chains  # noqa: F401
 
 __version__ = '0.1.0'

@@ -481,6 +481,21 @@ def thin_chains(samples, gradients, n_points: int, standardize: bool = True, pre
     return greedy_concurrent([i.device_problem() for i in integrands], n_points, dedup=_dedup())
 
 
+def thin_gf_chains(samples, log_ps, log_qs, gradients_q, n_points: int, standardize: bool = True,
+                   range_cap: Optional[float] = None, preconditioner='id') -> list:
+    """``[thin_gf(s, lp, lq, gq, n_points, ...) for ...]`` with the thins side by side on one GPU
+    (see thin_chains); the same indices as the loop."""
+    from .device import greedy_concurrent
+    integrands = [_make_stein_gf_integrand(s, lp, lq, gq, standardize, range_cap, preconditioner)
+                  for s, lp, lq, gq in zip(samples, log_ps, log_qs, gradients_q)]
+    n_points = int(n_points)
+    if n_points < 0:
+        raise ValueError('negative dimensions are not allowed')
+    if n_points == 0:
+        raise IndexError('index 0 is out of bounds for axis 0 with size 0')
+    return greedy_concurrent([i.device_problem() for i in integrands], n_points, dedup=_dedup())
+
+
 def thin_gf(sample, log_p, log_q, gradient_q, n_points: int, standardize: bool = True,
             range_cap: Optional[float] = None, preconditioner='id') -> np.ndarray:
     """Gradient-free Stein thinning with auxiliary density q (report.tex:390-426)."""

@@ -186,3 +186,15 @@ def test_thin_chains_equal_the_per_chain_loop(dedup, monkeypatch):
     for a, b in zip(got, want):
         np.testing.assert_array_equal(a, b)
     np.testing.assert_array_equal(want[0], o.thin(chains[0][0], chains[0][1], 40, preconditioner='med'))
+
+
+def test_thin_gf_chains_equal_the_per_chain_loop():
+    chains = [_chain(30_000 + 500 * k, 3, seed=70 + k) for k in range(5)]
+    lps = [-0.5 * np.sum(x * x, axis=1) for x, _ in chains]
+    lqs = [-0.55 * np.sum(x * x, axis=1) for x, _ in chains]
+    got = stein_thinning.thin_gf_chains([c[0] for c in chains], lps, lqs, [c[1] for c in chains], 30,
+                                        preconditioner='med')
+    for (x, g), lp, lq, idx in zip(chains, lps, lqs, got):
+        np.testing.assert_array_equal(idx, st.thin_gf(x, lp, lq, g, 30, preconditioner='med'))
+    np.testing.assert_array_equal(got[0], o.thin_gf(chains[0][0], lps[0], lqs[0], chains[0][1], 30,
+                                                    preconditioner='med'))
