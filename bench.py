@@ -388,6 +388,8 @@ def main():
     ap.add_argument('--arith', default='compact', choices=['compact', 'exact'],
                     help='arithmetic of the d <= 8 greedy kernels (stein_thinning.set_arithmetic)')
     ap.add_argument('--chains', type=int, default=8, help='chains workload: independent chains thinned')
+    ap.add_argument('--batch', type=int, default=-1,
+                    help='chains workload: problems per st_greedy_batch launch (1 = streams only; -1 = device.BATCH)')
     ap.add_argument('--in-flight', type=int, default=-1,
                     help='chains workload: thins in flight at once (-1 = stein_thinning.device.IN_FLIGHT)')
     ap.add_argument('--workload', default='thin', choices=['thin', 'ksd', 'proxy', 'lv', 'energy', 'ranks', 'chains'],
@@ -688,11 +690,12 @@ def main_chains(args):
     probs = [st._make_stein_integrand(*lv_call_shape(n, 20_000 + k, 'exp'), preconditioner='med').device_problem()
              for k in mine]
     in_flight = args.in_flight if args.in_flight > 0 else sdev.IN_FLIGHT
+    batch = args.batch if args.batch > 0 else sdev.BATCH
 
-    def run(c):
+    def run(c, b=batch):
         for p in probs:
             p._dedup = False   # run detection inside the timed region
-        return sdev.greedy_concurrent(probs, m, in_flight=c)
+        return sdev.greedy_concurrent(probs, m, in_flight=c, batch=b)
     seq = run(1)
     for _ in range(args.warmup):
         run(in_flight)
@@ -705,13 +708,21 @@ def main_chains(args):
         got = run(in_flight)
         torch.cuda.synchronize()
         times.append(time.perf_counter() - t0)
+    streams_times = []
     for _ in range(2):
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         run(1)
         torch.cuda.synchronize()
         seq_times.append(time.perf_counter() - t0)
+        if batch > 1:   # the same on streams only (no batch launch), for comparison
+            t0 = time.perf_counter()
+            st_only = run(in_flight, 1)
+            torch.cuda.synchronize()
+            streams_times.append(time.perf_counter() - t0)
     same = all(np.array_equal(a, b) for a, b in zip(got, seq))
+    if streams_times:
+        same = same and all(np.array_equal(a, b) for a, b in zip(st_only, seq))
     elapsed = float(np.median(times))
     if world > 1:
         elapsed = _max_over_ranks([elapsed], dev)[0]
@@ -722,11 +733,12 @@ def main_chains(args):
                 'vs_baseline': None, 'dtype': 'f64',
                 'data': 'synthetic (seeded RW-MH LV-surrogate chains, one per seed; see bench.py lv_call_shape)',
                 'config': {'workload': f"{args.chains} chains x thin(np.exp(s), grads, 10_000, 'med')",
-                           'n_per_chain': n, 'm': m, 'in_flight': in_flight,
+                           'n_per_chain': n, 'm': m, 'in_flight': in_flight, 'batch': batch,
                            'run_starts': [p.dedup_view().n_unique if p.dedup_view() is not None else p.n for p in probs],
                            'parallelism': f'chains dealt to {world} ranks' if world > 1 else 'single-gpu'},
                 'one_after_the_other_ms': round(float(np.median(seq_times)) * 1e3, 2),
                 'side_by_side_ms': round(elapsed * 1e3, 2),
+                'streams_only_ms': round(float(np.median(streams_times)) * 1e3, 2) if streams_times else None,
                 'same_indices_as_one_after_the_other': bool(same)}
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -164,6 +164,45 @@ int st_greedy(const double* x_soa, const double* g_soa, const double* weights, i
                            n_points, idx_out, a_work, workspace, workspace_bytes, stream);
 }
 
+int st_greedy_batch(int32_t count, const double* const* x_soa, const double* const* g_soa,
+                    const double* const* weights, const int64_t* n, int32_t d, const int64_t* ld,
+                    const double* linv_scale, const double* linv_trace, int64_t n_points,
+                    uint32_t* const* idx_out, double* const* a_work, void* const* workspace,
+                    const int64_t* workspace_bytes, void* stream) {
+    if (count < 1 || count > st::kMaxBatchProblems)
+        return fail(ST_ERR_INVALID, "count must be in [1, %d]", st::kMaxBatchProblems);
+    if (!x_soa || !g_soa || !n || !ld || !linv_scale || !linv_trace || !idx_out || !a_work || !workspace ||
+        !workspace_bytes)
+        return fail(ST_ERR_INVALID, "NULL argument array");
+    if (n_points < 1) return fail(ST_ERR_INVALID, "n_points must be >= 1");
+    st::BatchProblem pr[st::kMaxBatchProblems];
+    for (int q = 0; q < count; ++q) {
+        const double* w = weights ? weights[q] : nullptr;
+        if ((w == nullptr) != (!weights || weights[0] == nullptr))
+            return fail(ST_ERR_INVALID, "problem %d: weights must be given for every problem or none", q);
+        int rc = check_problem(x_soa[q], g_soa[q], w, n[q], d, ld[q]);
+        if (rc) return rc;
+        if (!idx_out[q] || !a_work[q] || !workspace[q])
+            return fail(ST_ERR_INVALID, "problem %d: NULL output/workspace", q);
+        if (!aligned16(a_work[q]) || !aligned16(workspace[q]))
+            return fail(ST_ERR_INVALID, "problem %d: a_work/workspace must be 16-byte aligned", q);
+        if (workspace_bytes[q] < greedy_ws_bytes(d))
+            return fail(ST_ERR_INVALID, "problem %d: workspace too small (%lld < %lld)", q,
+                        (long long)workspace_bytes[q], (long long)greedy_ws_bytes(d));
+        pr[q] = st::BatchProblem{x_soa[q], g_soa[q], w, a_work[q], n[q], ld[q], linv_scale[q], linv_trace[q],
+                                 idx_out[q], workspace[q], workspace_bytes[q]};
+    }
+    int used = 0;
+    const hipError_t e = st::launch_greedy_persistent_batch(count, pr, d, n_points, static_cast<hipStream_t>(stream),
+                                                            &used);
+    if (used) return ST_OK;
+    if (e == hipErrorNotSupported)
+        return fail(ST_ERR_UNSUPPORTED, "batch launch does not apply (d = 2 / 4, every problem on the 512-thread "
+                    "kernel with the same register rows at #CU / count blocks); run st_greedy per problem");
+    (void)hipGetLastError();
+    return hip_check(e, "batch persistent launch");
+}
+
 int64_t st_mailbox_bytes(int32_t nranks) {
     if (nranks < 1 || nranks > st::kMailboxRanks) return -1;
     return st::kMailboxBytes;

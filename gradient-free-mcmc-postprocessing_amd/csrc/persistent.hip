@@ -23,6 +23,7 @@
 // Arithmetic per pair: K2's (stein_math.hpp) or, when the block's rows and the winner lie in the
 // guarded range, its division/sqrt-light form that returns the same bits (finish_pair_fast):
 // results are bit-identical to st_greedy's launch-per-step path and to the C bit model.
+#include <algorithm>
 #include <type_traits>
 
 #include "stein_math.hpp"
@@ -294,7 +295,7 @@ __device__ __forceinline__ void combine_waves(const Scratch* sc, uint64_t& k, ui
 
 template <int NT>
 __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, double v, uint32_t row,
-                                        int64_t t, int64_t r1) {
+                                        int64_t t, int64_t r1, unsigned bid) {
     // padding rows (>= r1) carry +inf and the "no row" sentinel index, so they lose every tie --
     // their indices may be real rows of the next rank
     int64_t li = (int64_t)row < r1 ? (int64_t)row : INT64_MAX;
@@ -311,7 +312,7 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
             uint32_t ib;
             combine_waves<NT>(sc, k, ib);
             sc->vblk = key_value(k);   // read by every thread after wait_and_pick's barrier
-            uint64_t* gr = a.gran + (t & 1) * a.rep_stride + (int64_t)blockIdx.x * a.rec_stride;
+            uint64_t* gr = a.gran + (t & 1) * a.rep_stride + (int64_t)bid * a.rec_stride;
             const uint64_t tag = step_tag(t);
             __hip_atomic_store(gr + 0, tag | (k >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(gr + 1, tag | ((k & 0xFFull) << 32) | ib, __ATOMIC_RELAXED,
@@ -329,7 +330,7 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
             const uint64_t tag = step_tag(t);
             const uint64_t g0 = tag | (k >> 8), g1 = tag | ((k & 0xFFull) << 32) | ib;
             const int64_t off = (((t & 1) * a.nrep + threadIdx.x) * a.rep_stride +
-                                 (int64_t)blockIdx.x * a.rec_stride) * 8;
+                                 (int64_t)bid * a.rec_stride) * 8;
             const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(a.gran, 0, 0x7FFFFFFF, 0x00020000);
             typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)g0, (unsigned)(g0 >> 32), (unsigned)g1,
@@ -365,17 +366,17 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 // writes the row to sc->row.  Returns the winner's index, or -1 if the sweep timed out (grid-wide
 // abort).
 template <int D, bool GF, int MAXG>
-__device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t) {
+__device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* sc, int64_t t, unsigned bid,
+                                                 const int G) {
     static_assert(MAXG % 64 == 0 && MAXG <= kMaxGrid && MAXG / 64 <= 32, "records per lane");
     constexpr bool kWide = D > kMaxCtDim;
     // wide rows are not prefetched into registers (2d + 1 doubles per lane): the wave loads the
     // winner's row into LDS after the pick
     constexpr int kRow = kWide ? 1 : 2 * D + (GF ? 1 : 0);
-    const int G = gridDim.x;
     ST_STAMP(a, t + 1, 0);
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const uint64_t* bank = a.gran + ((t & 1) * a.nrep + (int)blockIdx.x % a.nrep) * a.rep_stride;
+        const uint64_t* bank = a.gran + ((t & 1) * a.nrep + (int)bid % a.nrep) * a.rep_stride;
         const uint64_t want = step_tag(t);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         const uint64_t wait_limit = (t == 0 && a.nranks == 1) ? kFirstStepTimeoutTicks : kTimeoutTicks;
@@ -559,7 +560,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             const uint64_t rtag = ((seq + 1) & 0xFFFFull) << 48;
             const int64_t mbank = (int64_t)(seq & 1) * kMaxRanks * 2;
             const uint32_t lib = gi == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)gi;
-            if (blockIdx.x == 0 && lane == 0) {
+            if (bid == 0 && lane == 0) {
                 const uint64_t vb = (uint64_t)__double_as_longlong(v);
                 const uint64_t g0 = rtag | (vb >> 16);
                 const uint64_t g1 = rtag | ((vb & 0xFFFFull) << 32) | lib;
@@ -661,8 +662,36 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
 // or the winner out of range, a NaN running sum) sets status 2 and every block leaves; the general
 // kernel, enqueued right behind it with gate = that status word, then runs the whole thin (and
 // returns at once when the compact-only run completed).  One device only.
-template <int D, bool GF, int RT, int NT, int BPC, bool CMP, bool GEN = true>
-__global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
+//
+// KA = BatchArgs: the batch launch (st_greedy_batch) -- independent thins in ONE launch, problem q
+// on the blocks [blk_begin[q], blk_begin[q + 1]), each group running exactly as a plain launch of
+// that many blocks would: its own records, status word and indices; the groups never read each
+// other's memory.  The thins then run side by side whatever hardware queues streams would map to.
+// (The body stays in the kernel itself: moved into a device function, the compact-only kernel
+// spilled 22 VGPRs instead of 8.)
+constexpr int kMaxBatch = kMaxBatchProblems;
+struct BatchArgs {
+    PersistArgs p[kMaxBatch];
+    int blk_begin[kMaxBatch + 1];
+    int count;
+};
+
+template <int D, bool GF, int RT, int NT, int BPC, bool CMP, bool GEN = true, typename KA = PersistArgs>
+__global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
+    constexpr bool kBatch = std::is_same<KA, BatchArgs>::value;
+    int grp = 0;   // the block's group
+    if constexpr (kBatch)
+        for (int k = 1; k < ka.count; ++k) grp += (int)blockIdx.x >= ka.blk_begin[k];
+    const PersistArgs& a = [&]() -> const PersistArgs& {
+        if constexpr (kBatch) return ka.p[grp]; else return ka;
+    }();
+    // the block's place in its group and the group's size (plain launch: the builtins)
+    auto bid = [&]() -> unsigned {
+        if constexpr (kBatch) return blockIdx.x - (unsigned)ka.blk_begin[grp]; else return blockIdx.x;
+    };
+    auto G = [&]() -> int {
+        if constexpr (kBatch) return ka.blk_begin[grp + 1] - ka.blk_begin[grp]; else return (int)gridDim.x;
+    };
     static_assert(!CMP || D <= kMaxCtDim, "compact arithmetic: d <= 8 only");
     static_assert(GEN || CMP, "the compact-only kernel is a compact kernel");
     if (a.gate && *a.gate != 2u) return;   // general kernel behind a compact-only run that finished
@@ -691,7 +720,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
     double* const sA = srow0 + (int64_t)(RL >> 6) * (kLF * 64);
     const int tid = threadIdx.x;
     const int64_t ld = a.ld;
-    const int64_t r0 = a.row_begin + (int64_t)blockIdx.x * a.rows_per_block;
+    const int64_t r0 = a.row_begin + (int64_t)bid() * a.rows_per_block;
     const int64_t r1 = (r0 + a.rows_per_block < a.row_end) ? r0 + a.rows_per_block : a.row_end;
     const int64_t lds_base = r0 + (int64_t)RT * kPBlock;
     const int64_t str_base = lds_base + RL;
@@ -787,14 +816,14 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             scan_take(kv, (uint32_t)row, bv, bi);
         }
     }
-    publish<NT>(a, sc, bv, bi, 0, r1);
+    publish<NT>(a, sc, bv, bi, 0, r1, bid());
 
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
     int64_t t = 1;
     for (; t < a.m; ++t) {
-        const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, t - 1);
+        const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, t - 1, bid(), G());
         if (win < 0) break;
-        if (blockIdx.x == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
+        if (bid() == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
         // chunk counter of the NEXT step (its last use, step t - 1, ended before publish's barrier)
         if (kDyn && tid == 0) sc->ctr[(t + 1) & 1] = 0;
         // small d: the winner row in SGPRs (VALU fp64 ops take one scalar operand); wide d: read
@@ -1085,19 +1114,19 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(PersistArgs a) {
             sweep_rows(std::integral_constant<int, CMP ? 3 : 0>{});
         }
         ST_STAMP(a, t, 3);
-        publish<NT>(a, sc, bv, bi, t, r1);
+        publish<NT>(a, sc, bv, bi, t, r1, bid());
         ST_STAMP(a, t, 4);
     }
     int64_t done = t;   // idx[0 .. done-1) are written
     if (t == a.m) {
-        const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, a.m - 1);
+        const int64_t win = wait_and_pick<D, GF, kMaxG>(a, sc, a.m - 1, bid(), G());
         if (win >= 0) {
-            if (blockIdx.x == 0 && tid == 0) a.idx_out[a.m - 1] = (uint32_t)win;
+            if (bid() == 0 && tid == 0) a.idx_out[a.m - 1] = (uint32_t)win;
             done = a.m + 1;
         }
     }
     // timeout: poison the unwritten indices (UINT32_MAX) so the host detects the failure
-    if (done <= a.m && blockIdx.x == 0)
+    if (done <= a.m && bid() == 0)
         for (int64_t q = (done > 0 ? done - 1 : 0) + tid; q < a.m; q += kPBlock) a.idx_out[q] = 0xFFFFFFFFu;
 
     // ---- write the on-chip running sums back (A_out contract of st_greedy) --------------------
@@ -1236,17 +1265,30 @@ int persistent_tune(int key, int value) {
     return -1;
 }
 
+// b != nullptr: the batch kernel over b's problems (G = every group's blocks together); it is
+// instantiated for the 512-thread one-block-per-CU kernels with the compact arithmetic only
 template <int D, bool GF, int RT, int NT, int BPC = 1, bool GEN = true>
-static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s, bool dry) {
+static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s, bool dry,
+                           const BatchArgs* b = nullptr) {
     // the compact instantiation for d <= 8 when st_tune key 11 selects it (the default); GEN = false:
     // the compact-only kernel (launch_greedy_persistent enqueues the general one behind it)
-    void (*fn)(PersistArgs);
-    if constexpr (!GEN) fn = greedy_persistent<D, GF, RT, NT, BPC, true, false>;
-    else if constexpr (D <= kMaxCtDim)
-        fn = arith_compact() ? greedy_persistent<D, GF, RT, NT, BPC, true> : greedy_persistent<D, GF, RT, NT, BPC, false>;
-    else fn = greedy_persistent<D, GF, RT, NT, BPC, false>;
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(fn),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    const void* fn;
+    if (b) {
+        if constexpr (NT == 512 && BPC == 1 && D <= kMaxCtDim) {
+            if (!arith_compact()) return hipErrorNotSupported;
+            fn = reinterpret_cast<const void*>(greedy_persistent<D, GF, RT, NT, BPC, true, GEN, BatchArgs>);
+        } else {
+            return hipErrorNotSupported;
+        }
+    } else if constexpr (!GEN) {
+        fn = reinterpret_cast<const void*>(greedy_persistent<D, GF, RT, NT, BPC, true, false>);
+    } else if constexpr (D <= kMaxCtDim) {
+        fn = arith_compact() ? reinterpret_cast<const void*>(greedy_persistent<D, GF, RT, NT, BPC, true>)
+                             : reinterpret_cast<const void*>(greedy_persistent<D, GF, RT, NT, BPC, false>);
+    } else {
+        fn = reinterpret_cast<const void*>(greedy_persistent<D, GF, RT, NT, BPC, false>);
+    }
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
     // co-residency of the whole grid (every block spins on the others' records): checked here
     // against the occupancy query -- what hipLaunchCooperativeKernel would check at launch -- and
@@ -1260,36 +1302,40 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     int dev = 0, cus = 0, per_cu = 0;
     if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
     if ((e = hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
-    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void*>(fn), NT, lds)) !=
-        hipSuccess)
+    if ((e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, NT, lds)) != hipSuccess)
         return e;
     if ((int64_t)per_cu * cus < G) return hipErrorNotSupported;
     if (dry) return hipSuccess;
     PersistArgs args = a;
-    void* kargs[] = {&args};
-    return hipLaunchKernel(reinterpret_cast<const void*>(fn), dim3(G), dim3(NT), kargs, lds, s);
+    BatchArgs bargs;
+    if (b) bargs = *b;
+    void* kargs[] = {b ? static_cast<void*>(&bargs) : static_cast<void*>(&args)};
+    return hipLaunchKernel(fn, dim3(G), dim3(NT), kargs, lds, s);
 }
 
 // compact-only kernels: 512-thread blocks, 8 / 9 / 10 register rows per thread
 template <int D, bool GF>
-static hipError_t launch_p_cmp(const PersistArgs& a, int rt, int G, size_t lds, hipStream_t s, bool dry) {
-    if (rt >= 10) return launch_p<D, GF, 10, 512, 1, false>(a, G, lds, s, dry);
-    if (rt == 9) return launch_p<D, GF, 9, 512, 1, false>(a, G, lds, s, dry);
-    return launch_p<D, GF, 8, 512, 1, false>(a, G, lds, s, dry);
+static hipError_t launch_p_cmp(const PersistArgs& a, int rt, int G, size_t lds, hipStream_t s, bool dry,
+                               const BatchArgs* b) {
+    if (rt >= 10) return launch_p<D, GF, 10, 512, 1, false>(a, G, lds, s, dry, b);
+    if (rt == 9) return launch_p<D, GF, 9, 512, 1, false>(a, G, lds, s, dry, b);
+    return launch_p<D, GF, 8, 512, 1, false>(a, G, lds, s, dry, b);
 }
 
 template <int D, bool GF>
 static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int G, size_t lds, hipStream_t s,
-                               bool dry) {
+                               bool dry, const BatchArgs* b) {
     if (bpc == 2) {
+        if (b) return hipErrorNotSupported;
         if (rt <= 4) return launch_p<D, GF, 4, 256, 2>(a, G, lds, s, dry);
         return launch_p<D, GF, 8, 256, 2>(a, G, lds, s, dry);
     }
     if (nt == 512) {
-        if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s, dry);
-        if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s, dry);
-        return launch_p<D, GF, 8, 512>(a, G, lds, s, dry);
+        if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s, dry, b);
+        if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s, dry, b);
+        return launch_p<D, GF, 8, 512>(a, G, lds, s, dry, b);
     }
+    if (b) return hipErrorNotSupported;   // batch: the 512-thread kernels only
     switch (rt) {
         case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s, dry);
         case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s, dry);
@@ -1298,24 +1344,39 @@ static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int
 }
 
 static hipError_t launch_cmp(const PersistArgs& a, int d, bool gf, int rt, int G, size_t lds, hipStream_t s,
-                             bool dry) {
-    if (d == 2) return gf ? launch_p_cmp<2, true>(a, rt, G, lds, s, dry) : launch_p_cmp<2, false>(a, rt, G, lds, s, dry);
-    return gf ? launch_p_cmp<4, true>(a, rt, G, lds, s, dry) : launch_p_cmp<4, false>(a, rt, G, lds, s, dry);
+                             bool dry, const BatchArgs* b = nullptr) {
+    if (d == 2) return gf ? launch_p_cmp<2, true>(a, rt, G, lds, s, dry, b) : launch_p_cmp<2, false>(a, rt, G, lds, s, dry, b);
+    return gf ? launch_p_cmp<4, true>(a, rt, G, lds, s, dry, b) : launch_p_cmp<4, false>(a, rt, G, lds, s, dry, b);
 }
 
 static hipError_t launch_kind(const PersistArgs& a, int d, bool wide, bool gf, int rt, int nt, int bpc, int G,
-                              size_t lds, hipStream_t s, bool dry) {
-    if (wide) return gf ? launch_p<kWideD, true, 1, 256>(a, G, lds, s, dry) : launch_p<kWideD, false, 1, 256>(a, G, lds, s, dry);
-    if (d == 2) return gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s, dry) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s, dry);
-    return gf ? launch_p_rt<4, true>(a, rt, nt, bpc, G, lds, s, dry) : launch_p_rt<4, false>(a, rt, nt, bpc, G, lds, s, dry);
+                              size_t lds, hipStream_t s, bool dry, const BatchArgs* b = nullptr) {
+    if (wide) {
+        if (b) return hipErrorNotSupported;
+        return gf ? launch_p<kWideD, true, 1, 256>(a, G, lds, s, dry) : launch_p<kWideD, false, 1, 256>(a, G, lds, s, dry);
+    }
+    if (d == 2) return gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s, dry, b) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s, dry, b);
+    return gf ? launch_p_rt<4, true>(a, rt, nt, bpc, G, lds, s, dry, b) : launch_p_rt<4, false>(a, rt, nt, bpc, G, lds, s, dry, b);
 }
 
-// Returns hipErrorNotSupported when the persistent path does not apply (caller falls back).
-hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
-                                    int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
-                                    uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
-                                    int* used, const RankSpec* rs, bool plan_only) {
-    *used = 0;
+namespace {
+// one thin's launch decision: the kernel instantiation(s), grid, LDS and arguments
+struct Plan {
+    PersistArgs a, ac;     // general kernel / compact-only kernel (use_cmp)
+    bool wide, gf, use_cmp, own_region;
+    int d, rt, nt, bpc, G, rt_c;
+    size_t lds, lds_c;
+    int64_t region;        // bytes of one record region
+    char* ws;
+};
+}  // namespace
+
+// Everything up to the launches; hipErrorNotSupported when the persistent path does not apply.
+// plan_only: the eligibility query (every pointer may be a placeholder); *used = 1 if it applies.
+static hipError_t plan_persistent(const double* x, const double* g, const double* w, double* A, int64_t n,
+                                  int d, int64_t ld, double l, double tr, int64_t m, uint32_t* idx_out,
+                                  void* ws, int64_t ws_bytes, hipStream_t s, int* used, const RankSpec* rs,
+                                  bool plan_only, int grid_cap, Plan& P) {
     const RankSpec one{0, n, 0, 1, 0, nullptr, {}};
     if (!rs) rs = &one;
     // 32-bit row indices, padding rows included (< n + one block's register rows)
@@ -1340,7 +1401,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     int nt = wide ? 256 : (g_persist_nt > 0 ? g_persist_nt : 256);
     const int bpc = (!wide && nt == 256 && g_persist_bpc == 2) ? 2 : 1;
     int G = cus * bpc > kMaxGrid ? kMaxGrid : cus * bpc;
-    if (g_persist_grid > 0 && G > g_persist_grid) G = g_persist_grid;
+    if (grid_cap > 0 && G > grid_cap) G = grid_cap;
     const int64_t min_rows = 256;   // fewer blocks for small n: exchange cost grows with G
     if (n_shard < (int64_t)G * min_rows) G = (int)((n_shard + min_rows - 1) / min_rows);
     if (G < 1) G = 1;
@@ -1455,22 +1516,104 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     // record region of its own when the workspace holds one (st_greedy_workspace_bytes does), else
     // the shared region is zeroed again between the two launches.
     const int64_t region = persistent_region_bytes(G, pitch, nrep);
-    const bool own_region = use_cmp && kWsControlBytes + 2 * region <= ws_bytes;
-    // zero status and every granule tag (a stale tag from a previous run must never match)
-    hipError_t e = hipMemsetAsync(p, 0, (size_t)(kWsControlBytes + (own_region ? 2 : 1) * region), s);
-    if (e != hipSuccess) return e;
-    if (use_cmp) {
-        e = launch_cmp(ac, d, gf, rt_c, G, lds_c, s, false);
-        if (e != hipSuccess) return e;
-        a.gate = ac.status;
-        a.status = ac.status + 1;
-        if (own_region) {
-            a.gran = reinterpret_cast<uint64_t*>(p + kWsControlBytes + region);
-        } else if ((e = hipMemsetAsync(p + kWsControlBytes, 0, (size_t)region, s)) != hipSuccess) {
+    P.a = a;
+    P.ac = ac;
+    P.wide = wide; P.gf = gf; P.use_cmp = use_cmp;
+    P.own_region = use_cmp && kWsControlBytes + 2 * region <= ws_bytes;
+    P.d = d; P.rt = rt; P.nt = nt; P.bpc = bpc; P.G = G; P.rt_c = rt_c;
+    P.lds = lds; P.lds_c = lds_c;
+    P.region = region;
+    P.ws = p;
+    return hipSuccess;
+}
+
+// zero status and every granule tag (a stale tag from a previous run must never match); with the
+// compact-only kernel, point the general kernel's gate / status / records past the compact run's
+static hipError_t prepare_ws(Plan& P, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(P.ws, 0, (size_t)(kWsControlBytes + (P.own_region ? 2 : 1) * P.region), s);
+    if (e != hipSuccess || !P.use_cmp) return e;
+    P.a.gate = P.ac.status;
+    P.a.status = P.ac.status + 1;
+    if (P.own_region) P.a.gran = reinterpret_cast<uint64_t*>(P.ws + kWsControlBytes + P.region);
+    return hipSuccess;
+}
+
+// Returns hipErrorNotSupported when the persistent path does not apply (caller falls back).
+hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
+                                    int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
+                                    uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
+                                    int* used, const RankSpec* rs, bool plan_only) {
+    *used = 0;
+    Plan P;
+    hipError_t e = plan_persistent(x, g, w, A, n, d, ld, l, tr, m, idx_out, ws, ws_bytes, s, used, rs, plan_only,
+                                   g_persist_grid, P);
+    if (e != hipSuccess || plan_only) return e;
+    if ((e = prepare_ws(P, s)) != hipSuccess) return e;
+    if (P.use_cmp) {
+        if ((e = launch_cmp(P.ac, P.d, P.gf, P.rt_c, P.G, P.lds_c, s, false)) != hipSuccess) return e;
+        // the shared record region is zeroed again between the two launches (see above)
+        if (!P.own_region && (e = hipMemsetAsync(P.ws + kWsControlBytes, 0, (size_t)P.region, s)) != hipSuccess)
             return e;
-        }
     }
-    e = launch_kind(a, d, wide, gf, rt, nt, bpc, G, lds, s, false);
+    e = launch_kind(P.a, P.d, P.wide, P.gf, P.rt, P.nt, P.bpc, P.G, P.lds, s, false);
+    if (e == hipSuccess) *used = 1;
+    return e;
+}
+
+// Independent single-device thins in one launch (st_greedy_batch): each planned as a plain launch
+// capped at #CU / count blocks; all plans must pick the same 512-thread kernel (d, weights, register
+// rows), else hipErrorNotSupported (the caller runs them one by one).  The gated general kernel
+// behind a compact-only batch is a batch launch too: a group whose compact run completed returns at
+// once.
+hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int d, int64_t m, hipStream_t s,
+                                          int* used) {
+    *used = 0;
+    if (count < 1 || count > kMaxBatch || g_persist_rt == 0) return hipErrorNotSupported;
+    int dev = 0, cus = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        return hipErrorNotSupported;
+    int cap = cus / count;
+    if (g_persist_grid > 0 && cap > g_persist_grid) cap = g_persist_grid;
+    if (cap < 1) return hipErrorNotSupported;
+    Plan P[kMaxBatch];
+    BatchArgs bc{}, bg{};
+    bc.count = bg.count = count;
+    size_t lds = 0, lds_c = 0;
+    for (int q = 0; q < count; ++q) {
+        int u = 0;
+        hipError_t e = plan_persistent(pr[q].x, pr[q].g, pr[q].w, pr[q].A, pr[q].n, d, pr[q].ld, pr[q].l, pr[q].tr,
+                                       m, pr[q].idx_out, pr[q].ws, pr[q].ws_bytes, s, &u, nullptr, false, cap, P[q]);
+        if (e != hipSuccess) return e;
+        const Plan& p0 = P[0];
+        if (P[q].wide || P[q].nt != 512 || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].rt != p0.rt ||
+            P[q].use_cmp != p0.use_cmp || (p0.use_cmp && P[q].rt_c != p0.rt_c))
+            return hipErrorNotSupported;
+        P[q].a.stamps = P[q].ac.stamps = nullptr;
+        bc.blk_begin[q + 1] = bg.blk_begin[q + 1] = bc.blk_begin[q] + P[q].G;
+        lds = std::max(lds, P[q].lds);
+        lds_c = std::max(lds_c, P[q].lds_c);
+    }
+    const int G = bc.blk_begin[count];
+    const Plan& p0 = P[0];
+    // residency and the kernel's existence for this combination, before anything is enqueued
+    if (launch_kind(p0.a, d, false, p0.gf, p0.rt, 512, 1, G, lds, s, true, &bg) != hipSuccess ||
+        (p0.use_cmp && launch_cmp(p0.ac, d, p0.gf, p0.rt_c, G, lds_c, s, true, &bc) != hipSuccess))
+        return hipErrorNotSupported;
+    hipError_t e;
+    for (int q = 0; q < count; ++q) {
+        if ((e = prepare_ws(P[q], s)) != hipSuccess) return e;
+        bc.p[q] = P[q].ac;
+        bg.p[q] = P[q].a;
+    }
+    if (p0.use_cmp) {
+        if ((e = launch_cmp(p0.ac, d, p0.gf, p0.rt_c, G, lds_c, s, false, &bc)) != hipSuccess) return e;
+        for (int q = 0; q < count; ++q)
+            if (!P[q].own_region &&
+                (e = hipMemsetAsync(P[q].ws + kWsControlBytes, 0, (size_t)P[q].region, s)) != hipSuccess)
+                return e;
+    }
+    e = launch_kind(p0.a, d, false, p0.gf, p0.rt, 512, 1, G, lds, s, false, &bg);
     if (e == hipSuccess) *used = 1;
     return e;
 }

@@ -71,6 +71,21 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
                                     uint32_t* idx_out, void* ws, int64_t ws_bytes, hipStream_t s,
                                     int* used, const RankSpec* ranks = nullptr, bool plan_only = false);
+// one thin of a batch launch (st_greedy_batch): the st_greedy arguments of one problem
+struct BatchProblem {
+    const double* x;
+    const double* g;
+    const double* w;
+    double* A;
+    int64_t n, ld;
+    double l, tr;
+    uint32_t* idx_out;
+    void* ws;
+    int64_t ws_bytes;
+};
+constexpr int kMaxBatchProblems = 8;
+hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* problems, int d, int64_t m,
+                                          hipStream_t s, int* used);
 hipError_t launch_mailbox_handshake(const MailboxPeers& peers, uint64_t* inbox, int rank,
                                     int nranks, uint64_t token, int* ok, hipStream_t s);
 hipError_t launch_greedy_step(const GreedyArgs& a, bool diag, int blocks, hipStream_t s);

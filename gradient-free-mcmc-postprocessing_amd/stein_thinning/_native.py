@@ -37,6 +37,9 @@ SIGNATURES = {
     'st_tune': (ctypes.c_int, [_i32, _i32]),
     'st_greedy': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64, _i64,
                                  _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
+    # arrays of per-problem pointers / sizes (host arrays, see st_greedy_batch)
+    'st_greedy_batch': (ctypes.c_int, [_i32, _c_dp, _c_dp, _c_dp, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _i64,
+                                       _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
     'st_greedy_steps': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64, _i64,
                                        _i64, _i64, _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
     'st_greedy_step': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,

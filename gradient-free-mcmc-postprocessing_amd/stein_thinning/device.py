@@ -375,14 +375,45 @@ class DeviceProblem:
 # m = 10 000, repeated rows dropped, run detection included) took 83 ms with 4 in flight (64-block
 # grids) and 156 ms with 2, against 258-264 ms one after the other (profiles/r04_chains_probe.log)
 IN_FLIGHT = 4
+# problems per st_greedy_batch launch (at most 8): ONE launch runs them side by side on #CU / k
+# blocks each, whatever hardware queues streams would map to
+BATCH = 8
 
 
-def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, dedup=True) -> list:
+def _launch_batch(runs, n_points: int, bufs) -> bool:
+    """st_greedy_batch over ``runs`` (same d, all weighted or none) on the current stream; False when
+    the batch kernel does not apply to them (nothing enqueued)."""
+    import ctypes
+    L = nat.lib()
+    k = len(runs)
+
+    def arr(ctype, vals):
+        return (ctype * k)(*vals)
+    vp = ctypes.c_void_p
+    weighted = runs[0].w is not None
+    rc = L.st_greedy_batch(
+        k, arr(vp, [p.x.data_ptr() for p in runs]), arr(vp, [p.g.data_ptr() for p in runs]),
+        arr(vp, [p.w.data_ptr() for p in runs]) if weighted else None,
+        arr(ctypes.c_int64, [p.n for p in runs]), runs[0].d, arr(ctypes.c_int64, [p.ld for p in runs]),
+        arr(ctypes.c_double, [p.l for p in runs]), arr(ctypes.c_double, [p.tr for p in runs]), int(n_points),
+        arr(vp, [b[0].data_ptr() for b in bufs]), arr(vp, [b[1].data_ptr() for b in bufs]),
+        arr(vp, [b[2].data_ptr() for b in bufs]), arr(ctypes.c_int64, [b[2].numel() * 8 for b in bufs]),
+        nat.stream_handle())
+    if rc == nat.ST_ERR_UNSUPPORTED:
+        return False
+    nat.check(rc, 'st_greedy_batch')
+    return True
+
+
+def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, dedup=True,
+                      batch: Optional[int] = None) -> list:
     """Independent greedy thins on ONE GPU at the same time (the reference thins every MCMC chain on
     its own: Stein_thinning.ipynb, fan-out code/src/utils/parallel.py:48-52).  Each problem's launch
     runs on one of ``in_flight`` streams with a grid of #CU / in_flight blocks (st_tune key 5, restored
     afterwards), so that many latency-bound thins share the chip instead of queueing behind each
-    other.  Every result equals
+    other.  First, groups of up to ``batch`` (default BATCH) problems of one d go to the device as
+    ONE launch each (st_greedy_batch); groups the batch kernel does not take use the streams.
+    Every result equals
     ``problem.greedy(n_points, dedup=dedup)``; a launch whose bounded waits expired anyway (another
     process's kernels held CUs) is re-run alone.  Returns one uint32 index array per problem."""
     import torch
@@ -404,22 +435,38 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
                 v = None
         views.append(v)
     runs = [v.problem if v is not None else p for p, v in zip(problems, views)]
+    cur = torch.cuda.current_stream()
+    bufs, streams = [None] * k, [None] * k
+    kb = max(1, min(8, batch if batch is not None else BATCH))
+    if kb > 1:   # batch launches over groups of one d (and weights or none), in order
+        groups = {}
+        for i, p in enumerate(runs):
+            groups.setdefault((p.d, p.w is not None), []).append(i)
+        for ids in groups.values():
+            for j in range(0, len(ids), kb):
+                part = ids[j:j + kb]
+                if len(part) < 2:
+                    continue
+                b = [runs[i].greedy_buffers(n_points) for i in part]
+                if _launch_batch([runs[i] for i in part], n_points, b):
+                    for i, bi in zip(part, b):
+                        bufs[i], streams[i] = bi, cur
+    rest = [i for i in range(k) if bufs[i] is None]
+    c = max(1, min(len(rest), c))
     # c streams, problem i on stream i % c: at most c grids of #CU / c blocks are ever resident
     # together, so every grid fits beside the others
-    cur = torch.cuda.current_stream()
-    pool = [torch.cuda.Stream(device=runs[0].device) for _ in range(c)]
+    pool = [torch.cuda.Stream(device=runs[0].device) for _ in range(c)] if rest else []
     for s in pool:
         s.wait_stream(cur)   # the problems' arrays were written on the current stream
-    bufs, streams = [], []
-    nat.check(L.st_tune(5, max(1, cus // c)), 'st_tune')
+    if rest:
+        nat.check(L.st_tune(5, max(1, cus // c) if c > 1 else -1), 'st_tune')
     try:
-        for i, p in enumerate(runs):
-            s = pool[i % c]
+        for j, i in enumerate(rest):
+            s = pool[j % c]
             with torch.cuda.stream(s):
-                b = p.greedy_buffers(n_points)
-                p.greedy_launch(n_points, *b)
-            bufs.append(b)
-            streams.append(s)
+                b = runs[i].greedy_buffers(n_points)
+                runs[i].greedy_launch(n_points, *b)
+            bufs[i], streams[i] = b, s
     finally:
         L.st_tune(5, -1)
     out = []

@@ -112,6 +112,23 @@ int st_greedy(const double *x_soa, const double *g_soa, const double *weights, i
               void *stream);
 
 /*
+ * Up to 8 independent whole greedy runs of one d (2 or 4) and one n_points in ONE launch of the
+ * persistent kernel: problem q gets about #CU / count blocks and runs on them exactly as st_greedy
+ * would on a grid of that many blocks -- idx_out[q] and a_work[q] as st_greedy's, same indices.
+ * The arrays are host arrays of count entries (device pointers / sizes per problem, as st_greedy
+ * takes them); weights is NULL or has an entry for every problem.  Returns ST_ERR_UNSUPPORTED
+ * (nothing enqueued) when the problems do not all plan onto the same 512-thread kernel at that grid
+ * (e.g. fewer than ~1300 rows per block); the caller then runs st_greedy per problem.  A timed-out
+ * run poisons its own idx_out only.  Replaces the reference's loop of thin() calls over chains
+ * (Stein_thinning.ipynb; code/src/utils/parallel.py:48-52 fans them out to processes).
+ */
+int st_greedy_batch(int32_t count, const double *const *x_soa, const double *const *g_soa,
+                    const double *const *weights, const int64_t *n, int32_t d, const int64_t *ld,
+                    const double *linv_scale, const double *linv_trace, int64_t n_points,
+                    uint32_t *const *idx_out, double *const *a_work, void *const *workspace,
+                    const int64_t *workspace_bytes, void *stream);
+
+/*
  * Steps [t_begin, t_end) of the same single-device run (t = 0 is the diagonal); when t_end ==
  * n_points the finalize kernel writing idx_out[n_points-1] follows.  The workspace carries the
  * per-block candidate records between calls, so consecutive ranges on one stream compose into

@@ -122,6 +122,28 @@ def test_host_side_validation_of_the_newer_entry_points(libpath):
     assert lib.st_layout_soa_scaled(p, 10, 4, 16, None, 1, p, None) == inv                 # no scale
     assert lib.st_pdist(p, 1, 4, p, None) == inv and lib.st_pdist(p, 70_000, 4, p, None) == inv
     assert lib.st_pdist(p, 10, 0, p, None) == inv and lib.st_pdist(None, 10, 4, p, None) == inv
+    # batch launch: count, NULL arrays, per-problem checks (weights for some problems only, ld % 8,
+    # workspace size) -- all before any HIP call
+    def arr(ctype, vals):
+        return (ctype * len(vals))(*vals)
+    P2 = arr(ctypes.c_void_p, [p.value, p.value])
+    N2, LD2 = arr(ctypes.c_int64, [10, 10]), arr(ctypes.c_int64, [16, 16])
+    F2 = arr(ctypes.c_double, [1.0, 1.0])
+    WS2 = arr(ctypes.c_int64, [1 << 24, 1 << 24])
+    batch = [2, P2, P2, None, N2, 4, LD2, F2, F2, 5, P2, P2, P2, WS2, None]
+    for k, bad in [(0, 0), (0, 9), (1, None), (6, None), (13, None), (9, 0)]:
+        a = list(batch)
+        a[k] = bad
+        assert lib.st_greedy_batch(*a) == inv, (k, bad)
+    a = list(batch)
+    a[3] = arr(ctypes.c_void_p, [p.value, None])                      # weights for one problem only
+    assert lib.st_greedy_batch(*a) == inv and b'weights' in lib.st_last_error()
+    a = list(batch)
+    a[6] = arr(ctypes.c_int64, [16, 12])                              # ld % 8
+    assert lib.st_greedy_batch(*a) == inv
+    a = list(batch)
+    a[13] = arr(ctypes.c_int64, [1 << 24, 8])                         # workspace too small
+    assert lib.st_greedy_batch(*a) == inv and b'problem 1' in lib.st_last_error()
 
 
 def test_library_is_gfx950_only(libpath):
