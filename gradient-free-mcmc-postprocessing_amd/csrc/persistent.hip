@@ -675,6 +675,7 @@ struct BatchArgs {
     int blk_begin[kMaxBatch + 1];
     int count;
 };
+static_assert(sizeof(BatchArgs) <= 4096, "kernel arguments are limited to 4 KB");
 
 template <int D, bool GF, int RT, int NT, int BPC, bool CMP, bool GEN = true, typename KA = PersistArgs>
 __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
