@@ -197,8 +197,8 @@ int st_greedy_batch(int32_t count, const double* const* x_soa, const double* con
                                                             &used);
     if (used) return ST_OK;
     if (e == hipErrorNotSupported)
-        return fail(ST_ERR_UNSUPPORTED, "batch launch does not apply (d = 2 / 4, every problem on the 512-thread "
-                    "kernel with the same register rows at #CU / count blocks); run st_greedy per problem");
+        return fail(ST_ERR_UNSUPPORTED, "batch launch does not apply (d = 2 / 4, every problem planned onto the same "
+                    "kernel -- threads per block, register rows -- at #CU / count blocks); run st_greedy per problem");
     (void)hipGetLastError();
     return hip_check(e, "batch persistent launch");
 }

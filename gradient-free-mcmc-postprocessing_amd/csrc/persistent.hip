@@ -1267,7 +1267,7 @@ int persistent_tune(int key, int value) {
 }
 
 // b != nullptr: the batch kernel over b's problems (G = every group's blocks together); it is
-// instantiated for the 512-thread one-block-per-CU kernels with the compact arithmetic only
+// instantiated for the one-block-per-CU kernels (256 and 512 threads) with the compact arithmetic only
 template <int D, bool GF, int RT, int NT, int BPC = 1, bool GEN = true>
 static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t s, bool dry,
                            const BatchArgs* b = nullptr) {
@@ -1275,7 +1275,7 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     // the compact-only kernel (launch_greedy_persistent enqueues the general one behind it)
     const void* fn;
     if (b) {
-        if constexpr (NT == 512 && BPC == 1 && D <= kMaxCtDim) {
+        if constexpr (BPC == 1 && D <= kMaxCtDim) {
             if (!arith_compact()) return hipErrorNotSupported;
             fn = reinterpret_cast<const void*>(greedy_persistent<D, GF, RT, NT, BPC, true, GEN, BatchArgs>);
         } else {
@@ -1336,11 +1336,10 @@ static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int
         if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s, dry, b);
         return launch_p<D, GF, 8, 512>(a, G, lds, s, dry, b);
     }
-    if (b) return hipErrorNotSupported;   // batch: the 512-thread kernels only
     switch (rt) {
-        case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s, dry);
-        case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s, dry);
-        default: return launch_p<D, GF, 16, 256>(a, G, lds, s, dry);
+        case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s, dry, b);
+        case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s, dry, b);
+        default: return launch_p<D, GF, 16, 256>(a, G, lds, s, dry, b);
     }
 }
 
@@ -1562,8 +1561,8 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
 }
 
 // Independent single-device thins in one launch (st_greedy_batch): each planned as a plain launch
-// capped at #CU / count blocks; all plans must pick the same 512-thread kernel (d, weights, register
-// rows), else hipErrorNotSupported (the caller runs them one by one).  The gated general kernel
+// capped at #CU / count blocks; all plans must pick the same kernel (d, weights, threads per block,
+// register rows), else hipErrorNotSupported (the caller runs them one by one).  The gated general kernel
 // behind a compact-only batch is a batch launch too: a group whose compact run completed returns at
 // once.
 hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int d, int64_t m, hipStream_t s,
@@ -1587,7 +1586,7 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
                                        m, pr[q].idx_out, pr[q].ws, pr[q].ws_bytes, s, &u, nullptr, false, cap, P[q]);
         if (e != hipSuccess) return e;
         const Plan& p0 = P[0];
-        if (P[q].wide || P[q].nt != 512 || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].rt != p0.rt ||
+        if (P[q].wide || P[q].nt != p0.nt || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].rt != p0.rt ||
             P[q].use_cmp != p0.use_cmp || (p0.use_cmp && P[q].rt_c != p0.rt_c))
             return hipErrorNotSupported;
         P[q].a.stamps = P[q].ac.stamps = nullptr;
@@ -1598,7 +1597,7 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
     const int G = bc.blk_begin[count];
     const Plan& p0 = P[0];
     // residency and the kernel's existence for this combination, before anything is enqueued
-    if (launch_kind(p0.a, d, false, p0.gf, p0.rt, 512, 1, G, lds, s, true, &bg) != hipSuccess ||
+    if (launch_kind(p0.a, d, false, p0.gf, p0.rt, p0.nt, 1, G, lds, s, true, &bg) != hipSuccess ||
         (p0.use_cmp && launch_cmp(p0.ac, d, p0.gf, p0.rt_c, G, lds_c, s, true, &bc) != hipSuccess))
         return hipErrorNotSupported;
     hipError_t e;
@@ -1614,7 +1613,7 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
                 (e = hipMemsetAsync(P[q].ws + kWsControlBytes, 0, (size_t)P[q].region, s)) != hipSuccess)
                 return e;
     }
-    e = launch_kind(p0.a, d, false, p0.gf, p0.rt, 512, 1, G, lds, s, false, &bg);
+    e = launch_kind(p0.a, d, false, p0.gf, p0.rt, p0.nt, 1, G, lds, s, false, &bg);
     if (e == hipSuccess) *used = 1;
     return e;
 }

@@ -117,8 +117,9 @@ int st_greedy(const double *x_soa, const double *g_soa, const double *weights, i
  * would on a grid of that many blocks -- idx_out[q] and a_work[q] as st_greedy's, same indices.
  * The arrays are host arrays of count entries (device pointers / sizes per problem, as st_greedy
  * takes them); weights is NULL or has an entry for every problem.  Returns ST_ERR_UNSUPPORTED
- * (nothing enqueued) when the problems do not all plan onto the same 512-thread kernel at that grid
- * (e.g. fewer than ~1300 rows per block); the caller then runs st_greedy per problem.  A timed-out
+ * (nothing enqueued) when the problems do not all plan onto the same kernel at that grid (threads
+ * per block and register rows follow each problem's rows per block, as in st_greedy; e.g. a 2e5-row
+ * problem next to a 2e4-row one); the caller then runs st_greedy per problem.  A timed-out
  * run poisons its own idx_out only.  Replaces the reference's loop of thin() calls over chains
  * (Stein_thinning.ipynb; code/src/utils/parallel.py:48-52 fans them out to processes).
  */

@@ -77,16 +77,30 @@ def test_batch_compact_only_and_handoff():
         assert np.array_equal(A, cA)
 
 
-def test_batch_declines_small_or_mixed_problems():
-    """Problems the batch kernel does not take (too few rows per block for the 512-thread kernel, or
-    different register rows) return ST_ERR_UNSUPPORTED with nothing enqueued."""
+@pytest.mark.parametrize('gf', [False, True])
+def test_batch_small_problems_256_thread_kernel(gf):
+    """Small problems (20k .. 60k rows: a few hundred rows per block, the 256-thread kernel) batch
+    too: indices and running sums equal each problem's own run."""
+    m = 25
+    inputs = [_problem(n, 2, seed=200 + k, gf=gf) for k, n in enumerate((20_000, 33_333, 47_001, 60_000))]
+    probs = [DeviceProblem(*inp) for inp in inputs]
+    applied, got = _batch(probs, m)
+    assert applied
+    for p, (idx, A) in zip(probs, got):
+        want, want_A = p.greedy(m, return_sums=True, dedup=False)
+        np.testing.assert_array_equal(idx, want)
+        assert np.array_equal(A, want_A), np.flatnonzero(A != want_A)[:10]
+
+
+def test_batch_declines_mixed_or_unsupported_problems():
+    """Problems that plan onto different kernels (a 2e4-row problem next to a 2e5-row one, or
+    different register rows), or a d the persistent kernel does not take, return ST_ERR_UNSUPPORTED
+    with nothing enqueued."""
     m = 20
-    small = [DeviceProblem(*_problem(20_000, 4, seed=k)) for k in range(3)]
-    applied, _ = _batch(small, m)
-    assert not applied
-    mixed = [DeviceProblem(*_problem(n, 4, seed=k)) for k, n in enumerate((150_000, 900_000))]
-    applied, _ = _batch(mixed, m)
-    assert not applied
+    for sizes, d in [((200_000, 20_000), 4), ((150_000, 900_000), 4), ((100_000, 100_000), 3)]:
+        probs = [DeviceProblem(*_problem(n, d, seed=k)) for k, n in enumerate(sizes)]
+        applied, _ = _batch(probs, m)
+        assert not applied, (sizes, d)
 
 
 def test_greedy_concurrent_batches_by_d(monkeypatch):
