@@ -387,7 +387,8 @@ def main():
                     help='energy kernel work units per launch (st_tune key 14; -1 = auto)')
     ap.add_argument('--arith', default='compact', choices=['compact', 'exact'],
                     help='arithmetic of the d <= 8 greedy kernels (stein_thinning.set_arithmetic)')
-    ap.add_argument('--chains', type=int, default=8, help='chains workload: independent chains thinned')
+    ap.add_argument('--chains', type=int, default=5,
+                    help='chains workload: independent chains thinned (5 = lotka_volterra.n_chains, code/src/lotka_volterra.py:67-75)')
     ap.add_argument('--batch', type=int, default=-1,
                     help='chains workload: problems per st_greedy_batch launch (1 = streams only; -1 = device.BATCH)')
     ap.add_argument('--in-flight', type=int, default=-1,
@@ -673,7 +674,8 @@ def thinned_sizes(n_points_calculate: int = 1000) -> np.ndarray:
 def main_chains(args):
     """The reference's per-chain LV thinning (Stein_thinning.ipynb cell 12: every RW-MH chain of
     n ~ 5e5 thinned on its own to m = 10 000 with 'med'; the fan-out is code/src/utils/parallel.py:48-52)
-    for `--chains` seeded surrogate chains (lv_call_shape 'exp'), standardised arrays resident on the
+    for `--chains` seeded surrogate chains (default 5, the reference's n_chains; lv_call_shape 'exp'),
+    standardised arrays resident on the
     GPU.  A step = all the chains' thins: one after the other (the loop the notebook runs) and side by
     side (stein_thinning.device.greedy_concurrent, each latency-bound thin on a share of the CUs);
     both drop repeated rows first (the drop-in thin's default), and the indices must agree.  `value`
