@@ -689,8 +689,8 @@ def main_chains(args):
         _init_group(dev)
     n, m = 500_000, 10_000
     mine = list(range(rank, args.chains, world))
-    probs = [st._make_stein_integrand(*lv_call_shape(n, 20_000 + k, 'exp'), preconditioner='med').device_problem()
-             for k in mine]
+    host = [lv_call_shape(n, 20_000 + k, 'exp') for k in mine]
+    probs = [st._make_stein_integrand(x, g, preconditioner='med').device_problem() for x, g in host]
     in_flight = args.in_flight if args.in_flight > 0 else sdev.IN_FLIGHT
     batch = args.batch if args.batch > 0 else sdev.BATCH
 
@@ -722,6 +722,19 @@ def main_chains(args):
             st_only = run(in_flight, 1)
             torch.cuda.synchronize()
             streams_times.append(time.perf_counter() - t0)
+    # end to end from host arrays (standardisation, upload, preconditioner, thin): the drop-in loop of
+    # thin() calls against thin_chains
+    import stein_thinning
+    e2e_loop, e2e_chains = [], []
+    for _ in range(2):
+        t0 = time.perf_counter()
+        loop_idx = [stein_thinning.thin(x, g, m, preconditioner='med') for x, g in host]
+        e2e_loop.append(time.perf_counter() - t0)
+        t0 = time.perf_counter()
+        ch_idx = stein_thinning.thin_chains([x for x, _ in host], [g for _, g in host], m, preconditioner='med')
+        e2e_chains.append(time.perf_counter() - t0)
+    same_e2e = all(np.array_equal(a, b) for a, b in zip(loop_idx, ch_idx)) and \
+        all(np.array_equal(a, b) for a, b in zip(loop_idx, seq))
     same = all(np.array_equal(a, b) for a, b in zip(got, seq))
     if streams_times:
         same = same and all(np.array_equal(a, b) for a, b in zip(st_only, seq))
@@ -741,6 +754,9 @@ def main_chains(args):
                 'one_after_the_other_ms': round(float(np.median(seq_times)) * 1e3, 2),
                 'side_by_side_ms': round(elapsed * 1e3, 2),
                 'streams_only_ms': round(float(np.median(streams_times)) * 1e3, 2) if streams_times else None,
+                'e2e_from_host_arrays_ms': {'loop_of_thin': round(min(e2e_loop) * 1e3, 2),
+                                            'thin_chains': round(min(e2e_chains) * 1e3, 2),
+                                            'same_indices': bool(same_e2e)},
                 'same_indices_as_one_after_the_other': bool(same)}
         print(json.dumps(line), flush=True)
     if world > 1:
