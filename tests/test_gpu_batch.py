@@ -128,3 +128,23 @@ def test_greedy_concurrent_batches_by_d(monkeypatch):
     for a, b in zip(got, want[:4]):
         np.testing.assert_array_equal(a, b)
     assert sorted(calls) == [(2, 2, True), (4, 2, True)]
+
+
+def test_thin_chains_raises_the_loops_error():
+    """thin_chains prepares the chains on host threads but raises what the loop of thin() calls
+    raises: the first failing chain's error (here chain 1's NaN, not chain 2's shape mismatch)."""
+    import re
+    import stein_thinning
+    rng = np.random.default_rng(9)
+    xs = [rng.normal(size=(70_000, 4)) for _ in range(4)]
+    gs = [-x for x in xs]
+    gs[1] = gs[1].copy()
+    gs[1][123, 2] = np.nan
+    gs[2] = gs[2][:, :3]
+    with pytest.raises(Exception) as want:
+        [stein_thinning.thin(x, g, 10, preconditioner='med') for x, g in zip(xs, gs)]
+    with pytest.raises(type(want.value), match=re.escape(str(want.value))):
+        stein_thinning.thin_chains(xs, gs, 10, preconditioner='med')
+    got = stein_thinning.thin_chains(xs[:1] + xs[3:], gs[:1] + gs[3:], 10, preconditioner='med')
+    for x, g, idx in zip(xs[:1] + xs[3:], gs[:1] + gs[3:], got):
+        np.testing.assert_array_equal(idx, stein_thinning.thin(x, g, 10, preconditioner='med'))
