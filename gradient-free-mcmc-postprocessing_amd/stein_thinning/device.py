@@ -412,7 +412,9 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
     runs on one of ``in_flight`` streams with a grid of #CU / in_flight blocks (st_tune key 5, restored
     afterwards), so that many latency-bound thins share the chip instead of queueing behind each
     other.  First, groups of up to ``batch`` (default BATCH) problems of one d go to the device as
-    ONE launch each (st_greedy_batch); groups the batch kernel does not take use the streams.
+    ONE launch each (st_greedy_batch); a group of 4 or more that the batch kernel declines (its
+    problems plan onto different kernels) is split into its smaller and larger half, each tried
+    again; what is left uses the streams.
     Every result equals
     ``problem.greedy(n_points, dedup=dedup)``; a launch whose bounded waits expired anyway (another
     process's kernels held CUs) is re-run alone.  Returns one uint32 index array per problem."""
@@ -438,19 +440,24 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
     cur = torch.cuda.current_stream()
     bufs, streams = [None] * k, [None] * k
     kb = max(1, min(8, batch if batch is not None else BATCH))
+    def try_batch(part):
+        if len(part) < 2:
+            return
+        b = [runs[i].greedy_buffers(n_points) for i in part]
+        if _launch_batch([runs[i] for i in part], n_points, b):
+            for i, bi in zip(part, b):
+                bufs[i], streams[i] = bi, cur
+        elif len(part) >= 4:   # declined (plans differ): the smaller and the larger half on their own
+            by_n = sorted(part, key=lambda i: runs[i].n)
+            try_batch(by_n[:len(by_n) // 2])
+            try_batch(by_n[len(by_n) // 2:])
     if kb > 1:   # batch launches over groups of one d (and weights or none), in order
         groups = {}
         for i, p in enumerate(runs):
             groups.setdefault((p.d, p.w is not None), []).append(i)
         for ids in groups.values():
             for j in range(0, len(ids), kb):
-                part = ids[j:j + kb]
-                if len(part) < 2:
-                    continue
-                b = [runs[i].greedy_buffers(n_points) for i in part]
-                if _launch_batch([runs[i] for i in part], n_points, b):
-                    for i, bi in zip(part, b):
-                        bufs[i], streams[i] = bi, cur
+                try_batch(ids[j:j + kb])
     rest = [i for i in range(k) if bufs[i] is None]
     c = max(1, min(len(rest), c))
     # c streams, problem i on stream i % c: at most c grids of #CU / c blocks are ever resident

@@ -148,3 +148,24 @@ def test_thin_chains_raises_the_loops_error():
     got = stein_thinning.thin_chains(xs[:1] + xs[3:], gs[:1] + gs[3:], 10, preconditioner='med')
     for x, g, idx in zip(xs[:1] + xs[3:], gs[:1] + gs[3:], got):
         np.testing.assert_array_equal(idx, stein_thinning.thin(x, g, 10, preconditioner='med'))
+
+
+def test_greedy_concurrent_splits_a_declined_batch(monkeypatch):
+    """Two large and two small problems of one d plan onto different kernels as one batch; the
+    declined group is split by size and each half goes out as its own batch launch."""
+    calls = []
+    real = device._launch_batch
+
+    def spy(runs, n_points, bufs):
+        ok = real(runs, n_points, bufs)
+        calls.append((len(runs), tuple(sorted(p.n for p in runs)), ok))
+        return ok
+    monkeypatch.setattr(device, '_launch_batch', spy)
+    m = 30
+    probs = [DeviceProblem(*_problem(n, 4, seed=300 + k)) for k, n in
+             enumerate([200_000, 20_000, 215_000, 25_000])]
+    got = device.greedy_concurrent(probs, m, dedup=False)
+    for p, idx in zip(probs, got):
+        np.testing.assert_array_equal(idx, p.greedy(m, dedup=False))
+    assert calls == [(4, (20_000, 25_000, 200_000, 215_000), False), (2, (20_000, 25_000), True),
+                     (2, (200_000, 215_000), True)]
