@@ -2,7 +2,7 @@
 # HBM traffic (rocprofv3 FETCH_SIZE / WRITE_SIZE, one counter per pass, each pass its own run) of
 # every bench workload's dominant kernel; summarised per launch into profiles/pmc_traffic.json by
 # tools/summarize_pmc.py (gfx950 FETCH_SIZE x2 correction).  Any failing pass ends the script.
-#   bash scripts/pmc_workloads.sh [key ...]      keys: energy ksd_c2 proxy_gauss proxy_t lv lv2 c4_persistent
+#   bash scripts/pmc_workloads.sh [key ...]      keys: energy ksd_c2 proxy_gauss proxy_t lv lv2 c4_persistent chains_batch
 # PMC_SOURCE (environment) labels the records (round, commit).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -10,11 +10,13 @@ mkdir -p gpurun_out/pmc
 export TMPDIR=/tmp
 declare -A ARGS=( [energy]="--workload energy" [ksd_c2]="--workload ksd" [proxy_gauss]="--workload proxy"
                   [proxy_t]="--workload proxy --proxy-kind t" [lv]="--workload lv"
-                  [c4_persistent]="--config c4 --no-kernel-timing" [lv2]="--workload lv" )
+                  [c4_persistent]="--config c4 --no-kernel-timing" [lv2]="--workload lv"
+                  [chains_batch]="--workload chains" )
 declare -A KERN=( [energy]="dist_colsum_kernel" [ksd_c2]="ksd_colsum_kernel" [proxy_gauss]="proxy_mfma_buf_kernel"
                   [proxy_t]="proxy_mfma_buf_kernel" [lv]="lv_kernel<10>"
-                  [c4_persistent]="greedy_persistent<4, false, 9, 512, 1, true, false, st::PersistArgs>" [lv2]="lv_dense_kernel" )
-declare -A EXCL=( [c4_persistent]="@none@" [lv2]="@none@" )
+                  [c4_persistent]="greedy_persistent<4, false, 9, 512, 1, true, false, st::PersistArgs>" [lv2]="lv_dense_kernel"
+                  [chains_batch]="st::BatchArgs>" )
+declare -A EXCL=( [c4_persistent]="@none@" [lv2]="@none@" [chains_batch]="@none@" )
 KEYS=("$@")
 [[ ${#KEYS[@]} -gt 0 ]] || KEYS=(energy ksd_c2 proxy_gauss proxy_t lv)
 for key in "${KEYS[@]}"; do
