@@ -279,7 +279,14 @@ def dedup_timing(prob, m: int, want_idx, stream, repeats: int = 5):
     torch.cuda.synchronize()
     med = float(np.median([e0.elapsed_time(e1) * 1e-3 for e0, e1 in evs]))
     got = view.to_rows(idx.cpu().numpy().view(np.uint32))
-    return {'used': True, 'drop_in_takes_it': bool(prob.dedup_pays(m) and prob.dedup_pays(m, sp.n)),
+    from stein_thinning import _native as nat
+    try:   # the near-tie guard's verdict on the run starts (the drop-in's path): -1 = no step flagged
+        tie = nat.near_tie_step(ws)
+    except nat.HipExtensionError:   # an older A/B build (ST_HIP_LIB) without the guard
+        tie = None
+    return {'used': True, 'drop_in_takes_it': bool(prob.guard_mode() == 'kernel' or
+                                                   (prob.dedup_pays(m) and prob.dedup_pays(m, sp.n))),
+            'near_tie_step': tie,
             'rows_kept': sp.n, 'of': prob.n, 'detect_s': round(det[-1], 6),
             'thin_s': round(med, 6), 's_per_thin_incl_detect': det[-1] + med,
             'pair_evals_per_thin': sp.n * m,
@@ -431,6 +438,11 @@ def main():
 
     cfg = CONFIGS[args.config]
     n, m = cfg['n'], cfg['m']
+    if os.environ.get('ST_TUNE'):   # measurement sweeps: "key=value,key=value" st_tune settings
+        from stein_thinning import _native as nat
+        for kv in os.environ['ST_TUNE'].split(','):
+            k, v = kv.split('=')
+            nat.check(nat.lib().st_tune(int(k), int(v)), 'ST_TUNE')
     integrand, host_x, host_g = make_integrand(cfg)
     d = integrand.sample.shape[1]
     import stein_thinning

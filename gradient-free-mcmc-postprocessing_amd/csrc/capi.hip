@@ -96,11 +96,18 @@ int st_tune(int32_t key, int32_t value) {
     else if (key == 14) rc = st::dist_units_tune(value);
     else if (key == 17) rc = st::lv_tune(value);
     else if (key == 18) rc = st::lv_pieces_tune(value);
-    else rc = ((key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12 || key == 15 || key == 16 || key == 19)
+    else rc = ((key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12 || key == 15 || key == 16 || key == 19 ||
+               key == 21)
                   ? st::persistent_tune(key, value)
                                                                                           : st::tune(key, value);
     if (rc != 0) return fail(ST_ERR_INVALID, "bad tuning key/value %d=%d", key, value);
     return ST_OK;
+}
+
+int32_t st_tune_get(int32_t key) {
+    const bool persist = (key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12 || key == 15 ||
+                         key == 16 || key == 19 || key == 21;
+    return persist ? st::persistent_tune_get(key) : st::tune_get(key);
 }
 
 int64_t st_candidate_stride(int32_t d) {
@@ -127,6 +134,12 @@ int st_greedy_steps(const double* x_soa, const double* g_soa, const double* weig
     st::GreedyArgs a = make_args(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, a_work);
     a.idx_out = idx_out;
     const int blocks = st::greedy_blocks(n, d);
+    if (t_begin == 0) {   // a run starts: no near-tie word of an earlier run may survive (step kernels: unguarded)
+        rc = hip_check(hipMemsetAsync(static_cast<char*>(workspace) + st::kWsTieOff, 0,
+                                      (size_t)(st::kWsBoundsOff + 40 - st::kWsTieOff), s),
+                       "near-tie words reset");
+        if (rc) return rc;
+    }
     for (int64_t t = t_begin; t < t_end; ++t) {
         a.t = t;
         a.recs_in = bank(workspace, d, (int)((t + 1) & 1));
@@ -162,6 +175,28 @@ int st_greedy(const double* x_soa, const double* g_soa, const double* weights, i
     if (pe != hipErrorNotSupported) (void)hipGetLastError();   // clear a failed launch
     return st_greedy_steps(x_soa, g_soa, weights, n, d, ld, linv_scale, linv_trace, 0, n_points,
                            n_points, idx_out, a_work, workspace, workspace_bytes, stream);
+}
+
+int st_greedy_near_tie(const void* workspace, int64_t workspace_bytes, int64_t* step_out, void* stream) {
+    if (!workspace || !step_out) return fail(ST_ERR_INVALID, "NULL workspace/output");
+    if (workspace_bytes < st::kWsControlBytes) return fail(ST_ERR_INVALID, "workspace too small");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    uint32_t w[12];   // status [0], [1] ... tie words [8 .. 11]
+    int rc = hip_check(hipMemcpyAsync(w, static_cast<const char*>(workspace) + st::kWsStatusOff, sizeof(w),
+                                      hipMemcpyDeviceToHost, s), "near-tie read-back");
+    if (rc) return rc;
+    rc = hip_check(hipStreamSynchronize(s), "near-tie read-back sync");
+    if (rc) return rc;
+    constexpr int kTie = (int)((st::kWsTieOff - st::kWsStatusOff) / 4);
+    if (w[kTie + 3] != 1u) {
+        *step_out = -2;
+        return ST_OK;
+    }
+    // the step kernels' word when they ran; else the gated general kernel's after a compact-only hand-off
+    // words hold ~step (atomic max over blocks = the first flagged step), 0 = none
+    const uint32_t tv = w[kTie + 2] ? w[kTie + 2] : (w[0] == 2u ? w[kTie + 1] : w[kTie]);
+    *step_out = tv ? (int64_t)(uint32_t)~tv : -1;
+    return ST_OK;
 }
 
 int st_greedy_batch(int32_t count, const double* const* x_soa, const double* const* g_soa,

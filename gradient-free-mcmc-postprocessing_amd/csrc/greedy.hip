@@ -437,13 +437,28 @@ static int g_cpt = -1;
 static int g_pf = -1;
 static int g_rt_max_blocks = kMaxBlocks;
 static int g_arith = 1;   // st_tune key 11
+static int g_tie_guard = 1;   // st_tune key 20
 constexpr int64_t kLargeShard = 1000000;
 
 int arith_compact() { return g_arith; }
+int tie_guard() { return g_tie_guard; }
+
+int tune_get(int key) {
+    switch (key) {
+        case 0: return g_max_blocks;
+        case 1: return g_cpt;
+        case 2: return g_pf;
+        case 6: return g_rt_max_blocks;
+        case 11: return g_arith;
+        case 20: return g_tie_guard;
+        default: return INT32_MIN;
+    }
+}
 
 int tune(int key, int value) {
     switch (key) {
         case 11: if (value < -1 || value > 1) return -1; g_arith = value < 0 ? 1 : value; return 0;
+        case 20: if (value < -1 || value > 1) return -1; g_tie_guard = value < 0 ? 1 : value; return 0;
         case 6: if (value < 1 || value > kMaxBlocks) return -1; g_rt_max_blocks = value; return 0;
         case 0: if (value < 1 || value > kMaxBlocks) return -1; g_max_blocks = value; return 0;
         case 1: if (value != -1 && value != 1 && value != 2 && value != 4) return -1; g_cpt = value; return 0;

@@ -524,10 +524,11 @@ hipError_t launch_lv(const LvArgs& a, bool gradient, hipStream_t s) {
         lv_kernel<10, true><<<blocks, kLvThreads, 0, s>>>(a);
         hipError_t e = hipGetLastError();
         if (e != hipSuccess) return e;
-        // observations in LDS when they fit the default 64 KB dynamic allocation (t_n <= 2730)
+        // observations in LDS when they fit next to the kernel's static LDS (pstart_sh: 8 x 65 ints) in
+        // the default 64 KB per block (t_n <= 2643; ADVICE r04: the static part counts too)
         const size_t obs_bytes = (size_t)a.t_n * 3 * sizeof(double);
         const int kp = g_lv_pieces > 0 ? g_lv_pieces : 1;
-        if (obs_bytes <= 65536 && g_lv_global_obs != 1) {
+        if (obs_bytes + sizeof(int) * 8 * 65 <= 65536 && g_lv_global_obs != 1) {
             const unsigned nb = (unsigned)((a.n + 7) / 8);
             if (kp == 2) lv_dense_kernel<8, true, 2><<<nb, 512, obs_bytes, s>>>(a);
             else if (kp == 3) lv_dense_kernel<8, true, 3><<<nb, 512, obs_bytes, s>>>(a);

@@ -129,3 +129,70 @@ extern "C" int st_standardize_upload(const double* sample, const double* gradien
     memcpy(scl_out, scl, (size_t)d * 8);
     return ST_OK;
 }
+
+// The reverse direction for samples that already live on the device (the drop-in thin called with ROCm
+// tensors): only x has to visit the host -- the column sums are one dependency chain of n adds per
+// column, which a CPU core runs ~8x faster than a GPU lane -- and g never leaves the device (its NaN /
+// inf flags are the caller's device reduction).  x comes back in 64 K-row chunks on `stream`, each
+// summed as it lands (NumPy's axis-0 order: acc[j] += x[i, j], row after row), then the absolute
+// deviations from loc in a second pass over the page-locked copy; the caller scales on the device
+// (st_layout_soa_scaled from the original device arrays).  *status: 0 ok, 1 NaN in x, 2 inf in x, 3 a
+// zero scale (x's flags only).  d = 2 .. 8 and n >= 65536 only (ST_ERR_UNSUPPORTED otherwise).
+extern "C" int st_standardize_download(const double* dev_x, int64_t n, int32_t d, double* stage_x, double* loc_out,
+                                       double* scl_out, int32_t* status, void* stream) {
+    if (!dev_x || !stage_x || !loc_out || !scl_out || !status)
+        return st::report_error(ST_ERR_INVALID, "st_standardize_download: NULL pointer");
+    if (d < 2 || d > 8 || n < 65536)
+        return st::report_error(ST_ERR_UNSUPPORTED, "st_standardize_download: d = 2 .. 8 and n >= 65536 only");
+    *status = 0;
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    constexpr int64_t kRows = 1 << 16;
+    const int64_t chunks = (n + kRows - 1) / kRows;
+    std::vector<hipEvent_t> ev((size_t)chunks, nullptr);
+    int rc = ST_OK;
+    for (int64_t c = 0; c < chunks && rc == ST_OK; ++c) {
+        const int64_t r0 = c * kRows, r1 = std::min(n, r0 + kRows);
+        if (hipEventCreateWithFlags(&ev[c], hipEventDisableTiming) != hipSuccess ||
+            hipMemcpyAsync(stage_x + r0 * d, dev_x + r0 * d, (size_t)(r1 - r0) * d * 8, hipMemcpyDeviceToHost, s) !=
+                hipSuccess ||
+            hipEventRecord(ev[c], s) != hipSuccess)
+            rc = ST_ERR_HIP;
+    }
+    double acc[8], l[8];
+    int fn = 0, fi = 0;
+    for (int64_t c = 0; c < chunks && rc == ST_OK; ++c) {
+        if (hipEventSynchronize(ev[c]) != hipSuccess) { rc = ST_ERR_HIP; break; }
+        const int64_t r0 = c * kRows, r1 = std::min(n, r0 + kRows);
+        for (int64_t i = r0; i < r1; ++i) {
+            const double* row = stage_x + i * d;
+            for (int j = 0; j < d; ++j) {
+                acc[j] = i == 0 ? row[j] : acc[j] + row[j];
+                fn |= (int)(row[j] != row[j]);
+                fi |= (int)(fabs(row[j]) == INFINITY);
+            }
+        }
+    }
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    if (rc != ST_OK) {
+        (void)hipStreamSynchronize(s);
+        return st::report_error(rc, "st_standardize_download: a device-to-host copy failed");
+    }
+    if (fn || fi) {
+        *status = fn ? 1 : 2;
+        return ST_OK;
+    }
+    const double dn = (double)n;
+    for (int j = 0; j < d; ++j) { l[j] = acc[j] / dn; acc[j] = fabs(stage_x[j] - l[j]); }
+    for (int64_t i = 1; i < n; ++i) {
+        const double* row = stage_x + i * d;
+        __builtin_prefetch(row + 64 * d);
+        for (int j = 0; j < d; ++j) acc[j] += fabs(row[j] - l[j]);
+    }
+    for (int j = 0; j < d; ++j) {
+        if (acc[j] / dn == 0.0) *status = 3;
+        loc_out[j] = l[j];
+        scl_out[j] = acc[j] / dn;
+    }
+    return ST_OK;
+}

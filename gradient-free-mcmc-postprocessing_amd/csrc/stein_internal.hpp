@@ -10,6 +10,15 @@ constexpr int kMaxCtDim = 8;     // compile-time-d kernels for d <= 8
 constexpr int kMaxBlocks = 1024; // greedy step grid cap (4 x 256-thread blocks per CU)
 constexpr int kCandHeader = 2;   // candidate record: {val, gidx(bits)} then x[d], g[d], w
 constexpr int64_t kWsControlBytes = 8 * 128 + 128;   // persistent kernel: arrival counters + status
+// control block words (byte offsets into the greedy workspace):
+constexpr int64_t kWsStatusOff = 8 * 128;   // u32 status: [0] persistent kernel, [1] the general kernel behind
+                                            // a compact-only run
+constexpr int64_t kWsTieOff = kWsStatusOff + 32;     // u32 near-tie words (first flagged step + 1, 0 = none):
+                                                     // [0] persistent kernel, [1] gated general kernel, [2] step
+                                                     // kernels; [3] = 1: the run is guarded (bounds computed)
+constexpr int64_t kWsBoundsOff = kWsStatusOff + 64;  // near-tie bounds: max_i |g_i|^2, max_i w_i^2 (f64 bits),
+                                                     // then the persistent run's final Q, E, thr (tests)
+static_assert(kWsBoundsOff + 40 <= kWsControlBytes, "control block layout");
 // peer mailbox (u64 words), one per rank, uncached device memory:
 //   [0, 32)        persistent kernel: 2 banks x kMailboxRanks slots x 2 tagged granules
 //   [32, 40)       handshake words (one per rank)
@@ -61,10 +70,14 @@ struct GreedyArgs {
 };
 
 int greedy_blocks(int64_t n, int d);
+// near-tie guard of the compact arithmetic (st_tune key 20: 1 = on, the default; 0 = off)
+int tie_guard();
 // st_tune key 11: arithmetic of the d <= 8 greedy kernels (1 = compact, the default; 0 = exact)
 int arith_compact();
 int tune(int key, int value);
 int persistent_tune(int key, int value);
+int persistent_tune_get(int key);
+int tune_get(int key);
 int64_t persistent_ws_bytes(int d, int G, int rec_stride, int nrep);
 int64_t persistent_ws_max_bytes();
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,

@@ -35,11 +35,13 @@ SIGNATURES = {
     'st_greedy_workspace_bytes': (_i64, [_i64, _i32, _i32]),
     'st_candidate_stride': (_i64, [_i32]),
     'st_tune': (ctypes.c_int, [_i32, _i32]),
+    'st_tune_get': (_i32, [_i32]),
     'st_greedy': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64, _i64,
                                  _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
     # arrays of per-problem pointers / sizes (host arrays, see st_greedy_batch)
     'st_greedy_batch': (ctypes.c_int, [_i32, _c_dp, _c_dp, _c_dp, _c_dp, _i32, _c_dp, _c_dp, _c_dp, _i64,
                                        _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
+    'st_greedy_near_tie': (ctypes.c_int, [_c_dp, _i64, ctypes.POINTER(_i64), _c_dp]),
     'st_greedy_steps': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64, _i64,
                                        _i64, _i64, _c_dp, _c_dp, _c_dp, _i64, _c_dp]),
     'st_greedy_step': (ctypes.c_int, [_c_dp, _c_dp, _c_dp, _i64, _i32, _i64, _f64, _f64,
@@ -56,6 +58,7 @@ SIGNATURES = {
     'st_layout_soa': (ctypes.c_int, [_c_dp, _i64, _i32, _i64, _c_dp, _c_dp]),
     'st_pdist': (ctypes.c_int, [_c_dp, _i64, _i32, _c_dp, _c_dp]),
     'st_layout_soa_scaled': (ctypes.c_int, [_c_dp, _i64, _i32, _i64, _c_dp, _i32, _c_dp, _c_dp]),
+    'st_standardize_download': (ctypes.c_int, [_c_dp, _i64, _i32, _c_dp, _c_dp, _c_dp, _c_dp, _c_dp]),
     'st_standardize_upload': (ctypes.c_int, [_c_dp, _c_dp, _i64, _i32, _c_dp, _c_dp, _c_dp, _c_dp,
                                              _c_dp, _c_dp, _c_dp, _c_dp]),
     'st_run_workspace_bytes': (_i64, [_i64]),
@@ -109,15 +112,26 @@ class HipExtensionError(RuntimeError):
     """The HIP extension is missing, failed to load, or reported an error."""
 
 
-def load_library(path: str = LIB_PATH) -> ctypes.CDLL:
-    """Load and type the C-ABI library (no GPU access: usable for symbol checks on CPU hosts)."""
+def load_library(path: str = LIB_PATH, partial: bool = False) -> ctypes.CDLL:
+    """Load and type the C-ABI library (no GPU access: usable for symbol checks on CPU hosts).
+    ``partial``: an older build of the same ABI (ST_HIP_LIB, same-box A/B timing) may lack newer entry
+    points; they raise when called."""
     if not os.path.exists(path):
         raise HipExtensionError(
             f'HIP extension not built: {path} is missing. Run `python -c "import __graft_entry__ as g; '
             f'g.build()"` from the repository root (hipcc --offload-arch=gfx950).')
     lib = ctypes.CDLL(path)
     for name, (res, args) in SIGNATURES.items():
-        fn = getattr(lib, name)
+        try:
+            fn = getattr(lib, name)
+        except AttributeError:
+            if not partial:
+                raise
+
+            def missing(*_a, _name=name):
+                raise HipExtensionError(f'{_name}: not in {path} (an older build)')
+            setattr(lib, name, missing)
+            continue
         fn.restype = res
         fn.argtypes = args
     if lib.st_abi_version() != ABI_VERSION:
@@ -133,7 +147,8 @@ def lib() -> ctypes.CDLL:
                 import torch  # noqa: F401  -- map torch's HIP runtime before ours resolves against it
                 # ST_HIP_LIB: another build of the same ABI (same-box A/B timing of a kernel change,
                 # scripts/ab_run.sh); the in-tree library otherwise
-                L = load_library(os.environ.get('ST_HIP_LIB') or LIB_PATH)
+                alt = os.environ.get('ST_HIP_LIB')
+                L = load_library(alt or LIB_PATH, partial=bool(alt))
                 mode = os.environ.get('ST_ARITH')
                 if mode:
                     if mode not in ARITHMETIC:
@@ -141,6 +156,7 @@ def lib() -> ctypes.CDLL:
                     L.st_tune(11, ARITHMETIC[mode])
                     global _ARITH
                     _ARITH = mode
+                L.st_tune(20, 1 if near_tie_guard() else 0)   # (an older A/B build rejects the key: harmless)
                 _LIB = L
     return _LIB
 
@@ -172,6 +188,55 @@ def set_arithmetic(mode: str) -> None:
     _ARITH = mode
 
 
+_GUARD = None   # set_near_tie_guard(); None: the ST_NEAR_TIE environment variable ('0' = off; on by default)
+
+
+def set_near_tie_guard(enabled) -> None:
+    """Near-tie guard of the compact arithmetic (st_tune key 20), on by default: a compact-arithmetic thin
+    whose selection at some step rests on sums closer than the arithmetic's error band is re-run with the
+    exact arithmetic, so the drop-in thin selects the reference NumPy path's rows.
+    True / False, or None to return to the ST_NEAR_TIE environment variable."""
+    global _GUARD
+    _GUARD = None if enabled is None else bool(enabled)
+    check(lib().st_tune(20, 1 if near_tie_guard() else 0), 'set_near_tie_guard')
+
+
+def near_tie_guard() -> bool:
+    if _GUARD is not None:
+        return _GUARD
+    return os.environ.get('ST_NEAR_TIE', '1') != '0'
+
+
+class arithmetic_override:
+    """``with arithmetic_override('exact'): ...`` -- the greedy kernels' arithmetic for the launches
+    enqueued inside the block (st_tune key 11 is process-wide; the previous mode is restored)."""
+
+    def __init__(self, mode: str):
+        if mode not in ARITHMETIC:
+            raise ValueError(f'arithmetic {mode!r}: expected one of {sorted(ARITHMETIC)}')
+        self.mode = mode
+
+    def __enter__(self):
+        self.prev = arithmetic()
+        if self.mode != self.prev:
+            set_arithmetic(self.mode)
+        return self
+
+    def __exit__(self, *exc):
+        if self.mode != self.prev:
+            set_arithmetic(self.prev)
+        return False
+
+
+def near_tie_step(ws) -> int:
+    """First flagged step of the completed greedy run whose workspace is ``ws`` (a device tensor), -1 when
+    none, -2 when the run was not guarded (st_greedy_near_tie; synchronises the current stream)."""
+    out = ctypes.c_int64(0)
+    check(lib().st_greedy_near_tie(ptr(ws), ws.numel() * ws.element_size(), ctypes.byref(out), stream_handle()),
+          'st_greedy_near_tie')
+    return int(out.value)
+
+
 def check_host(rc: int, what: str = '') -> None:
     if rc != ST_OK:
         raise ValueError(f'{what}: invalid arguments ({rc})')
@@ -187,14 +252,65 @@ def check(rc: int, what: str = '') -> None:
         raise HipExtensionError(f'{what}: HIP error ({rc}): {msg}')
 
 
+def select_device_index(count: int, env=None, worker: bool = False, pid: int = 0):
+    """The device policy of a process (pure: tests call it with a mocked device count):
+    * ``ST_DEVICE`` in the environment: that device (an index < count);
+    * else ``LOCAL_RANK`` (torchrun / torch.distributed.run: one process per GPU): LOCAL_RANK % count;
+    * else, in a worker process of a pool (joblib / loky / multiprocessing / Dask -- the reference fans
+      ``thin`` out over chains in such workers, ``code/src/utils/parallel.py:48-52``) with several
+      devices: pid % count, so that consecutive workers land on different GPUs;
+    * else None: the current torch device (cuda:0 unless the caller chose another).
+    Returns the device index or None."""
+    env = os.environ if env is None else env
+    v = env.get('ST_DEVICE')
+    if v is not None and v != '':
+        try:
+            idx = int(v)
+        except ValueError:
+            raise ValueError(f'ST_DEVICE={v!r}: expected a device index') from None
+        if not 0 <= idx < count:
+            raise ValueError(f'ST_DEVICE={idx}: only {count} HIP device(s) visible')
+        return idx
+    v = env.get('LOCAL_RANK')
+    if v is not None and v != '' and count > 0:
+        return int(v) % count
+    if worker and count > 1:
+        return pid % count
+    return None
+
+
+_DEVICE_POLICY_DONE = False
+
+
+def _pool_worker() -> bool:
+    import multiprocessing
+    return multiprocessing.parent_process() is not None
+
+
 def require_device():
-    """Return the torch device the engine runs on; raise if no HIP device is visible."""
+    """Return the torch device the engine runs on; raise if no HIP device is visible.  On first use the
+    process applies ``select_device_index`` (ST_DEVICE, LOCAL_RANK, or a pool worker's share of the GPUs)
+    with torch.cuda.set_device; without a policy it uses the current device, so ``with
+    torch.cuda.device(k)`` blocks are honoured."""
     import torch
     if not torch.cuda.is_available():
         raise HipExtensionError(
             'stein_thinning (MI355X engine) needs a HIP device: torch.cuda.is_available() is False. '
             'There is no CPU fallback.')
+    global _DEVICE_POLICY_DONE
+    if not _DEVICE_POLICY_DONE:
+        _DEVICE_POLICY_DONE = True
+        idx = select_device_index(torch.cuda.device_count(), os.environ, _pool_worker(), os.getpid())
+        if idx is not None and idx != torch.cuda.current_device():
+            torch.cuda.set_device(idx)
     return torch.device('cuda', torch.cuda.current_device())
+
+
+def policy_pinned() -> bool:
+    """True when the process's device comes from the policy (ST_DEVICE, LOCAL_RANK, a pool worker):
+    thin_chains then keeps every chain on that device instead of spreading them over all GPUs."""
+    import torch
+    return select_device_index(torch.cuda.device_count(), os.environ, _pool_worker(), os.getpid()) is not None
 
 
 def stream_handle():

@@ -8,6 +8,7 @@ an argmin.
 """
 from __future__ import annotations
 
+import contextlib
 import warnings
 from typing import Optional
 
@@ -220,52 +221,89 @@ class DeviceProblem:
             self.l, self.tr, 0, int(n_points), int(n_points), nat.ptr(idx), nat.ptr(a), nat.ptr(ws),
             ws.numel() * 8, nat.stream_handle()), 'st_greedy_steps')
 
-    def greedy(self, n_points: int, return_sums: bool = False, margins: bool = False, dedup=False):
+    def guard_mode(self, guard: bool = True) -> Optional[str]:
+        """How ``greedy(guard=True)`` -- the drop-in thin's call -- keeps the reference's selection under
+        the compact arithmetic (near-tie guard, on by default: nat.set_near_tie_guard / ST_NEAR_TIE): None
+        when nothing is needed (``guard`` False, the exact arithmetic, d > 8, or the guard is off); 'kernel'
+        for d = 2, 4 -- the persistent kernel flags a
+        step whose argmin rests on sums closer than the arithmetic's error band (st_greedy_near_tie) and
+        a flagged thin is re-run with the exact arithmetic; 'exact' for the other d <= 8, whose
+        launch-per-step kernels carry no flag: the thin runs with the exact arithmetic."""
+        if not guard or not nat.near_tie_guard() or self.d > 8 or nat.arithmetic() != 'compact':
+            return None
+        return 'kernel' if self.d in (2, 4) else 'exact'
+
+    def greedy(self, n_points: int, return_sums: bool = False, margins: bool = False, dedup=False,
+               guard: bool = False):
         """The reference's _greedy_search on the device.  ``self.fallback`` is None when the
         persistent launch completed, else why the run was repeated on the launch-per-step path
         (its bounded waits expired: the grid was not co-resident next to other work).
         ``margins=True``: (indices, diagnostics.GreedyMargins) -- the same selection with each step's
         argmin margin against the arithmetic's error band (launch-per-step kernels, one step at a time).
         ``dedup=True``: thin the run starts only (``dedup_view``) when repeated rows make that
-        worthwhile (``dedup_pays``); ``dedup='always'``: whenever dedup_view has a view.  Either way
-        the same indices and running sums bit for bit."""
+        worthwhile (``dedup_pays``) -- or, under the near-tie guard ('kernel' mode), whenever any row
+        repeats its predecessor, since the guard counts exact ties; ``dedup='always'``: whenever
+        dedup_view has a view.  Either way the same indices and running sums bit for bit.
+        ``guard=True`` (the drop-in thin): the near-tie guard (``guard_mode``); the indices are then the
+        reference NumPy path's even where the compact arithmetic alone would select another row, and
+        the sums those of whichever arithmetic ran.  ``self.near_tie``: the guard's verdict -- None (no
+        guard), -1 (no step flagged), t >= 0 (step t was flagged and the thin re-ran with the exact
+        arithmetic), -2 (the run carried no flag: it re-ran with the exact arithmetic)."""
         if margins:
             from .diagnostics import greedy_margins
             gm = greedy_margins(self, n_points)
             return gm.indices, gm
+        mode = self.guard_mode(guard)
         view = None
-        if dedup == 'always' or (dedup and self.dedup_pays(n_points)):
+        if mode == 'kernel' and dedup:
+            view = self.dedup_view(any_repeat=True)
+        elif dedup == 'always' or (dedup and self.dedup_pays(n_points)):
             view = self.dedup_view()
             if view is not None and dedup != 'always' and not self.dedup_pays(n_points, view.n_unique):
                 view = None
         self.dedup_used = view is not None
         if view is not None:
-            out, a = view.problem._greedy_run(n_points)
+            out, a = view.problem._greedy_run(n_points, mode)
             self.fallback = view.problem.fallback
+            self.near_tie = view.problem.near_tie
             out = view.to_rows(out)
             return (out, view.expand_sums(a)) if return_sums else out
-        out, a = self._greedy_run(n_points)
+        out, a = self._greedy_run(n_points, mode)
         return (out, a[:self.n].cpu().numpy()) if return_sums else out
 
-    def _greedy_run(self, n_points: int):
-        """(uint32 indices on the host, running sums on the device)."""
+    def _greedy_run(self, n_points: int, mode: Optional[str] = None):
+        """(uint32 indices on the host, running sums on the device).  ``mode``: guard_mode()'s value --
+        'exact' runs the exact arithmetic; 'kernel' reads the near-tie verdict of the compact run and
+        re-runs a flagged (or unflagged-capable: fallback) thin with the exact arithmetic."""
         idx, a, ws = self.greedy_buffers(n_points)
-        self.greedy_launch(n_points, idx, a, ws)
-        out = idx.cpu().numpy().view(np.uint32).copy()
+
+        def run(exact: bool):
+            with nat.arithmetic_override('exact') if exact else contextlib.nullcontext():
+                self.greedy_launch(n_points, idx, a, ws)
+                out = idx.cpu().numpy().view(np.uint32).copy()
+                if out.size and int(out.max()) >= self.n:
+                    self.fallback = ('persistent greedy kernel timed out (grid not co-resident?); '
+                                     're-ran on the launch-per-step kernels')
+                    warnings.warn(self.fallback, RuntimeWarning, stacklevel=4)
+                    self.greedy_steps_launch(n_points, idx, a, ws)
+                    out = idx.cpu().numpy().view(np.uint32).copy()
+                    if out.size and int(out.max()) >= self.n:
+                        raise nat.HipExtensionError('greedy step kernels returned out-of-range indices')
+            return out
+
         self.fallback = None
-        if out.size and int(out.max()) >= self.n:
-            self.fallback = ('persistent greedy kernel timed out (grid not co-resident?); '
-                             're-ran on the launch-per-step kernels')
-            warnings.warn(self.fallback, RuntimeWarning, stacklevel=3)
-            self.greedy_steps_launch(n_points, idx, a, ws)
-            out = idx.cpu().numpy().view(np.uint32).copy()
-            if out.size and int(out.max()) >= self.n:
-                raise nat.HipExtensionError('greedy step kernels returned out-of-range indices')
+        self.near_tie = None
+        out = run(mode == 'exact')
+        if mode == 'kernel':
+            self.near_tie = nat.near_tie_step(ws)
+            if self.near_tie != -1:   # flagged, or the run carried no flag (the step kernels' fallback)
+                out = run(True)
         return out, a
 
-    def dedup_view(self) -> Optional['DedupView']:
+    def dedup_view(self, any_repeat: bool = False) -> Optional['DedupView']:
         """The run starts of this problem as a compact problem, or None when fewer than
-        ``1 - DEDUP_MAX_FRAC`` of the rows repeat their predecessor (computed once, then cached).
+        ``1 - DEDUP_MAX_FRAC`` of the rows repeat their predecessor (``any_repeat``: when no row does);
+        computed once, then cached.
 
         A row that repeats the row before it bit for bit (x, g and w: a rejected MCMC proposal;
         about 77 % of the rows of a random-walk chain at the usual acceptance rate) has every pair
@@ -275,20 +313,25 @@ class DeviceProblem:
         sums are their run start's."""
         import torch
         cached = getattr(self, '_dedup', False)
-        if cached is not False:
-            return cached
-        view = None
-        if self.n > 1:
-            L = nat.lib()
-            starts = torch.empty(self.n, dtype=torch.uint8, device=self.device)
-            ws = torch.empty((int(L.st_run_workspace_bytes(self.n)) + 7) // 8, dtype=torch.int64, device=self.device)
-            nat.check(L.st_run_starts(nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.n, self.d, self.ld,
-                                      nat.ptr(starts), nat.ptr(ws), ws.numel() * 8, nat.stream_handle()),
-                      'st_run_starts')
-            count = int(ws[0].item())   # sizes the compact arrays
-            if count <= DEDUP_MAX_FRAC * self.n:
-                view = DedupView(self, starts, ws, count)
-        self._dedup = view
+        if cached is False:   # run detection, once
+            det = None
+            if self.n > 1:
+                L = nat.lib()
+                starts = torch.empty(self.n, dtype=torch.uint8, device=self.device)
+                ws = torch.empty((int(L.st_run_workspace_bytes(self.n)) + 7) // 8, dtype=torch.int64,
+                                 device=self.device)
+                nat.check(L.st_run_starts(nat.ptr(self.x), nat.ptr(self.g), nat.ptr(self.w), self.n, self.d,
+                                          self.ld, nat.ptr(starts), nat.ptr(ws), ws.numel() * 8,
+                                          nat.stream_handle()), 'st_run_starts')
+                det = [starts, ws, int(ws[0].item()), None]   # count sizes the compact arrays; the view
+            self._dedup = cached = det
+        if cached is None:
+            return None
+        starts, ws, count, view = cached
+        if count >= self.n or (not any_repeat and count > DEDUP_MAX_FRAC * self.n):
+            return None
+        if view is None:
+            view = cached[3] = DedupView(self, starts, ws, count)
         return view
 
     def dedup_pays(self, n_points: int, n_unique: Optional[int] = None) -> bool:
@@ -371,6 +414,8 @@ class DeviceProblem:
         return out.cpu().numpy()
 
 
+_GRID_CAP_LOCK = __import__('threading').Lock()
+
 # thins in flight at once in greedy_concurrent: 8 chains of the reference's LV call shape (5e5 rows,
 # m = 10 000, repeated rows dropped, run detection included) took 83 ms with 4 in flight (64-block
 # grids) and 156 ms with 2, against 258-264 ms one after the other (profiles/r04_chains_probe.log)
@@ -406,7 +451,7 @@ def _launch_batch(runs, n_points: int, bufs) -> bool:
 
 
 def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, dedup=True,
-                      batch: Optional[int] = None) -> list:
+                      batch: Optional[int] = None, guard: bool = False) -> list:
     """Independent greedy thins on ONE GPU at the same time (the reference thins every MCMC chain on
     its own: Stein_thinning.ipynb, fan-out code/src/utils/parallel.py:48-52).  Each problem's launch
     runs on one of ``in_flight`` streams with a grid of #CU / in_flight blocks (st_tune key 5, restored
@@ -416,7 +461,7 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
     problems plan onto different kernels) is split into its smaller and larger half, each tried
     again; what is left uses the streams.
     Every result equals
-    ``problem.greedy(n_points, dedup=dedup)``; a launch whose bounded waits expired anyway (another
+    ``problem.greedy(n_points, dedup=dedup, guard=guard)``; a launch whose bounded waits expired anyway (another
     process's kernels held CUs) is re-run alone.  Returns one uint32 index array per problem."""
     import torch
     problems = list(problems)
@@ -428,15 +473,23 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
     if c == 1:   # one at a time, full grid
         return [p.greedy(n_points, dedup=dedup) for p in problems]
     cus = torch.cuda.get_device_properties(problems[0].device).multi_processor_count
-    views = []
+    views, modes = [], []
     for p in problems:
         v = None
-        if dedup == 'always' or (dedup and p.dedup_pays(n_points)):
+        mode = p.guard_mode(guard)
+        if mode == 'kernel' and dedup:
+            v = p.dedup_view(any_repeat=True)
+        elif dedup == 'always' or (dedup and p.dedup_pays(n_points)):
             v = p.dedup_view()
             if v is not None and dedup != 'always' and not p.dedup_pays(n_points, v.n_unique):
                 v = None
         views.append(v)
+        modes.append(mode)
     runs = [v.problem if v is not None else p for p, v in zip(problems, views)]
+    for i, (p, mode) in enumerate(zip(runs, modes)):   # no near-tie flag on their kernels: exact, one by one
+        if mode == 'exact':
+            bufs_exact = p._greedy_run(n_points, 'exact')[0]
+            modes[i] = ('done', bufs_exact)
     cur = torch.cuda.current_stream()
     bufs, streams = [None] * k, [None] * k
     kb = max(1, min(8, batch if batch is not None else BATCH))
@@ -458,7 +511,7 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
         for ids in groups.values():
             for j in range(0, len(ids), kb):
                 try_batch(ids[j:j + kb])
-    rest = [i for i in range(k) if bufs[i] is None]
+    rest = [i for i in range(k) if bufs[i] is None and not isinstance(modes[i], tuple)]
     c = max(1, min(len(rest), c))
     # c streams, problem i on stream i % c: at most c grids of #CU / c blocks are ever resident
     # together, so every grid fits beside the others
@@ -466,21 +519,36 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
     for s in pool:
         s.wait_stream(cur)   # the problems' arrays were written on the current stream
     if rest:
-        nat.check(L.st_tune(5, max(1, cus // c) if c > 1 else -1), 'st_tune')
-    try:
-        for j, i in enumerate(rest):
-            s = pool[j % c]
-            with torch.cuda.stream(s):
-                b = runs[i].greedy_buffers(n_points)
-                runs[i].greedy_launch(n_points, *b)
-            bufs[i], streams[i] = b, s
-    finally:
-        L.st_tune(5, -1)
+        # the grid cap (st_tune key 5) is process-wide: set under a lock, the caller's value restored
+        with _GRID_CAP_LOCK:
+            prev = int(L.st_tune_get(5))
+            nat.check(L.st_tune(5, max(1, cus // c) if c > 1 else -1), 'st_tune')
+            try:
+                for j, i in enumerate(rest):
+                    s = pool[j % c]
+                    with torch.cuda.stream(s):
+                        b = runs[i].greedy_buffers(n_points)
+                        runs[i].greedy_launch(n_points, *b)
+                    bufs[i], streams[i] = b, s
+            finally:
+                L.st_tune(5, prev)
     out = []
-    for p, v, b, s in zip(runs, views, bufs, streams):
-        s.synchronize()
-        idx = b[0].cpu().numpy().view(np.uint32).copy()
-        if idx.size and int(idx.max()) >= p.n:   # not co-resident next to the others: alone now
-            idx, _ = p._greedy_run(n_points)
+    for p, v, b, s, mode in zip(runs, views, bufs, streams, modes):
+        if isinstance(mode, tuple):
+            idx = mode[1]
+        else:
+            s.synchronize()
+            idx = b[0].cpu().numpy().view(np.uint32).copy()
+            p.fallback, p.near_tie = None, None
+            if idx.size and int(idx.max()) >= p.n:   # not co-resident next to the others: alone now
+                p.fallback = 'the concurrent launch timed out (grid not co-resident?); re-ran alone'
+                idx, _ = p._greedy_run(n_points, mode)
+            elif mode == 'kernel':
+                with torch.cuda.stream(s):
+                    p.near_tie = nat.near_tie_step(b[2])
+                if p.near_tie != -1:   # flagged: the exact arithmetic decides (p.near_tie keeps the step)
+                    tie = p.near_tie
+                    idx, _ = p._greedy_run(n_points, 'exact')
+                    p.near_tie = tie
         out.append(v.to_rows(idx) if v is not None else idx)
     return out

@@ -234,6 +234,10 @@ class SteinIntegrand:
                 from .device import DeviceProblem
                 self._problem = DeviceProblem(self.sample, self.gradient, self.weights,
                                               self.linv_scale, self.linv_trace)
+                # a page-locked source is copied asynchronously, and torch records no event for a
+                # buffer it did not allocate: wait here, so the copy has landed whatever happens to the
+                # host arrays or the stream the problem is used on next
+                self._problem.wait_upload()
         return self._problem
 
     @contextlib.contextmanager
@@ -440,7 +444,8 @@ def _greedy_search(n_points: int, integrand: Callable) -> np.ndarray:
         if integrand._base is None and _rank_sharding():
             from .distributed import thin_across_ranks
             return thin_across_ranks(integrand, n_points)
-        return integrand.device_problem().greedy(n_points, dedup=_dedup())
+        from . import _native as nat
+        return integrand.device_problem().greedy(n_points, dedup=_dedup(), guard=nat.near_tie_guard())
     return _greedy_search_protocol(n_points, integrand)
 
 
@@ -460,40 +465,93 @@ def _dedup() -> bool:
     return _DEDUP if _DEDUP is not None else os.environ.get('ST_DEDUP', '1') != '0'
 
 
+def _guard() -> bool:
+    from . import _native as nat
+    return nat.near_tie_guard()
+
+
 def thin(sample, gradient, n_points: int, standardize: bool = True, preconditioner='id') -> np.ndarray:
     """Stein thinning: indices of ``n_points`` rows of ``sample`` greedily minimising the KSD."""
     integrand = _make_stein_integrand(sample, gradient, standardize, preconditioner)
     return _greedy_search(n_points, integrand)
 
 
-def thin_chains(samples, gradients, n_points: int, standardize: bool = True, preconditioner='id') -> list:
-    """``[thin(s, g, n_points, standardize, preconditioner) for s, g in zip(samples, gradients)]``
-    -- the reference's per-chain loop (Stein_thinning.ipynb) -- with the thins running side by side
-    on one GPU (device.greedy_concurrent: each latency-bound thin on a share of the CUs); the same
-    indices as the loop."""
+def _thin_chains(count: int, build: Callable, n_points) -> list:
+    """The per-chain loop ``[thin(...) for each chain]`` with the thins side by side: chain i's integrand is
+    ``build(i)`` (validation errors in the loop's order: chain 0's input, then n_points, then the other
+    chains'), the chains are dealt round-robin to the GPUs this process may use (all visible ones, or
+    the one the device policy pins: _native.select_device_index), and each GPU runs its chains with
+    device.greedy_concurrent (one batch launch: each latency-bound thin on a share of the CUs), the GPUs
+    at the same time.  The same indices as the loop."""
+    import torch
+    from . import _native as nat
     from .device import greedy_concurrent
-    integrands = [_make_stein_integrand(s, g, standardize, preconditioner) for s, g in zip(samples, gradients)]
     n_points = int(n_points)
-    if n_points < 0:
-        raise ValueError('negative dimensions are not allowed')
-    if n_points == 0:
-        raise IndexError('index 0 is out of bounds for axis 0 with size 0')
-    return greedy_concurrent([i.device_problem() for i in integrands], n_points, dedup=_dedup())
+    nat.require_device()
+    devs = ([torch.cuda.current_device()] if nat.policy_pinned() or count < 2
+            else list(range(torch.cuda.device_count())))
+    owner = [devs[i % len(devs)] for i in range(count)]
+    integrands = []
+    for i in range(count):
+        with torch.cuda.device(owner[i]):
+            integrands.append(build(i))
+        if i == 0:   # the loop's first thin() checks n_points after its input
+            if n_points < 0:
+                raise ValueError('negative dimensions are not allowed')
+            if n_points == 0:
+                raise IndexError('index 0 is out of bounds for axis 0 with size 0')
+    if count == 0:
+        return []
+    groups = {}
+    for i, dv in enumerate(owner):
+        groups.setdefault(dv, []).append(i)
+
+    def run(dv, ids):
+        with torch.cuda.device(dv):
+            return greedy_concurrent([integrands[i].device_problem() for i in ids], n_points, dedup=_dedup(),
+                                     guard=_guard())
+    out = [None] * count
+    if len(groups) == 1:
+        (dv, ids), = groups.items()
+        for i, r in zip(ids, run(dv, ids)):
+            out[i] = r
+        return out
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(max_workers=len(groups)) as ex:   # one host thread per GPU (HIP calls drop the GIL)
+        futs = {dv: ex.submit(run, dv, ids) for dv, ids in groups.items()}
+        for dv, ids in groups.items():
+            for i, r in zip(ids, futs[dv].result()):
+                out[i] = r
+    return out
+
+
+def _same_length(*lists) -> int:
+    n = len(lists[0])
+    if any(len(x) != n for x in lists[1:]):
+        raise ValueError('samples and gradients (and log densities) must have one entry per chain')
+    return n
+
+
+def thin_chains(samples, gradients, n_points: int, standardize: bool = True, preconditioner='id') -> list:
+    """``[thin(s, g, n_points, standardize, preconditioner) for s, g in zip(samples, gradients)]`` -- the
+    reference's per-chain loop (Stein_thinning.ipynb cells 12-14, fanned out over processes by
+    code/src/utils/parallel.py:48-52) -- with the thins side by side: on each GPU in one batch launch, and
+    over the visible GPUs (_thin_chains); the same indices as the loop."""
+    samples, gradients = list(samples), list(gradients)
+    count = _same_length(samples, gradients)
+    return _thin_chains(count, lambda i: _make_stein_integrand(samples[i], gradients[i], standardize,
+                                                               preconditioner), n_points)
 
 
 def thin_gf_chains(samples, log_ps, log_qs, gradients_q, n_points: int, standardize: bool = True,
                    range_cap: Optional[float] = None, preconditioner='id') -> list:
-    """``[thin_gf(s, lp, lq, gq, n_points, ...) for ...]`` with the thins side by side on one GPU
-    (see thin_chains); the same indices as the loop."""
-    from .device import greedy_concurrent
-    integrands = [_make_stein_gf_integrand(s, lp, lq, gq, standardize, range_cap, preconditioner)
-                  for s, lp, lq, gq in zip(samples, log_ps, log_qs, gradients_q)]
-    n_points = int(n_points)
-    if n_points < 0:
-        raise ValueError('negative dimensions are not allowed')
-    if n_points == 0:
-        raise IndexError('index 0 is out of bounds for axis 0 with size 0')
-    return greedy_concurrent([i.device_problem() for i in integrands], n_points, dedup=_dedup())
+    """``[thin_gf(s, lp, lq, gq, n_points, ...) for ...]`` with the thins side by side (see thin_chains);
+    the same indices as the loop."""
+    samples, log_ps, log_qs, gradients_q = list(samples), list(log_ps), list(log_qs), list(gradients_q)
+    count = _same_length(samples, log_ps, log_qs, gradients_q)
+    return _thin_chains(count, lambda i: _make_stein_gf_integrand(samples[i], log_ps[i], log_qs[i], gradients_q[i],
+                                                                  standardize, range_cap, preconditioner),
+                        n_points)
 
 
 def thin_gf(sample, log_p, log_q, gradient_q, n_points: int, standardize: bool = True,

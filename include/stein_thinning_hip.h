@@ -89,9 +89,14 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * 64 KB; same results), key 18 = LV gradient phase B: observation pieces per lane (1, 2, 3; -1 =
  * automatic; the per-point sum is reassociated differently, within the 1e-8 tolerance), key 19 =
  * 512-thread persistent kernels: two LDS-row chunks computed as two independent chains (1 / -1 =
- * automatic) or one after the other (0; same results).
+ * automatic) or one after the other (0; same results), key 20 = near-tie guard of the compact
+ * arithmetic (1 / -1 = on, the default; 0 = off; see st_greedy_near_tie; same indices and sums).
  */
 int st_tune(int32_t key, int32_t value);
+
+/* the current value of a greedy-kernel st_tune key (0 .. 6, 8 .. 12, 15, 16, 19, 20; -1 = automatic);
+ * INT32_MIN for other keys (save / restore around a temporary setting) */
+int32_t st_tune_get(int32_t key);
 
 /* doubles per rank-candidate record {value, global index bits, x[d], g[d], w} (even) */
 int64_t st_candidate_stride(int32_t d);
@@ -110,6 +115,23 @@ int st_greedy(const double *x_soa, const double *g_soa, const double *weights, i
               int32_t d, int64_t ld, double linv_scale, double linv_trace, int64_t n_points,
               uint32_t *idx_out, double *a_work, void *workspace, int64_t workspace_bytes,
               void *stream);
+
+/*
+ * Near-tie guard of the compact arithmetic (st_tune key 20).  A guarded run (one device, the compact
+ * arithmetic, d = 2 or 4; persistent kernel, batch included) flags the first step t whose selection the
+ * arithmetic could have decided differently from the reference's NumPy evaluation: the smallest running
+ * sum of any row other than the winner -- an exact tie included -- within thr(t) of the winner's, thr(t)
+ * a bound on how far two rows' sums may move between the compact arithmetic, the exact one and NumPy's
+ * (oracle/stein_ref.c sr_greedy_mt_ties states the rule and the bound; the reference's argmin is
+ * JAX_Stein_Thinning.ipynb:291-292, np.argmin of the running sums).  Exact ties count, so the guard is
+ * meant for problems without adjacent repeated rows (thin the run starts: st_run_starts /
+ * st_run_compact).  Reads the workspace of a completed st_greedy / st_greedy_batch problem after
+ * synchronising `stream` (the one exception to the enqueue-only rule: a few bytes come back):
+ * *step_out = the first flagged step, -1 when none, -2 when the run was not guarded (exact arithmetic,
+ * guard off, other d, a multi-rank run, or the launch-per-step kernels).  Callers re-run a flagged thin
+ * with the exact arithmetic (st_tune key 11 = 0).
+ */
+int st_greedy_near_tie(const void *workspace, int64_t workspace_bytes, int64_t *step_out, void *stream);
 
 /*
  * Up to 8 independent whole greedy runs of one d (2 or 4) and one n_points in ONE launch of the
@@ -393,6 +415,16 @@ int st_run_compact(const double *x_soa, const double *g_soa, const double *weigh
 int st_standardize_upload(const double *sample, const double *gradient, int64_t n, int32_t d,
                           double *stage_x, double *stage_g, double *dev_x, double *dev_g,
                           double *loc_out, double *scl_out, int32_t *status, void *stream);
+
+/* The device-resident counterpart (the drop-in thin called with ROCm tensors; replaces the reference's
+ * np.asarray of the inputs + _validate_and_standardize's statistics): x (row-major (n, d) on the device)
+ * comes back into the page-locked stage_x in 64 K-row chunks on `stream`, each chunk's column sums taken
+ * as it lands (NumPy's sequential axis-0 order, bit-identical); loc_out / scl_out as st_standardize_host's.
+ * g stays on the device (its NaN / inf check is the caller's).  *status: 0 ok, 1 NaN in x, 2 inf in x, 3 a
+ * zero scale.  d = 2 .. 8 and n >= 65536 only (ST_ERR_UNSUPPORTED otherwise).  Returns when x is on the
+ * host and the statistics are done. */
+int st_standardize_download(const double *dev_x, int64_t n, int32_t d, double *stage_x, double *loc_out,
+                            double *scl_out, int32_t *status, void *stream);
 
 /* row-major (n, d) -> SoA (d, ld) layout helper (device to device) */
 int st_layout_soa(const double *rowmajor, int64_t n, int32_t d, int64_t ld, double *soa,

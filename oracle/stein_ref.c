@@ -213,6 +213,9 @@ typedef struct {
     double *bv;
     int64_t *bi;
     pthread_barrier_t bar;
+    double *gap;   /* sr_greedy_mt_ties: per step, (smallest sum > the winner's) - (the winner's) */
+    double *rv;    /* per thread: its smallest sum above the step's winning value */
+    double *wv;    /* sr_greedy_mt_ties: per step, the winner's running sum */
 } mt_ctx;
 
 typedef struct { mt_ctx *c; int tid; } mt_arg;
@@ -252,19 +255,40 @@ static void *mt_worker(void *p) {
                 if (gb < 0 || better(c->bv[q], c->bi[q], gv, gb)) { gb = c->bi[q]; gv = c->bv[q]; }
             }
             c->idx[t] = (uint32_t)gb;
+            c->bv[0] = gv;
         }
         pthread_barrier_wait(&c->bar);
+        if (c->gap) {   /* the runner-up: smallest sum of any row other than the winner (ties count) */
+            const double gv = c->bv[0];
+            const int64_t wi = c->idx[t];
+            double r = INFINITY;
+            for (int64_t i = r0; i < r1; i++)
+                if (i != wi && c->A[i] < r) r = c->A[i];
+            c->rv[a->tid] = r;
+            pthread_barrier_wait(&c->bar);
+            if (a->tid == 0) {
+                double rr = INFINITY;
+                for (int q = 0; q < c->nthreads; q++) rr = c->rv[q] < rr ? c->rv[q] : rr;
+                c->gap[t] = rr - gv;
+                if (c->wv) c->wv[t] = gv;
+            }
+            pthread_barrier_wait(&c->bar);
+        }
     }
     return NULL;
 }
 
-int sr_greedy_mt(const double *x, const double *g, const double *w, int64_t n, int d,
-                 double l, double tr, int64_t m, uint32_t *idx, double *A, int nthreads, int arith) {
+static int greedy_mt(const double *x, const double *g, const double *w, int64_t n, int d,
+                     double l, double tr, int64_t m, uint32_t *idx, double *A, int nthreads, int arith,
+                     double *gap, double *wv) {
     if (d < 1 || d > 128 || n < 1) return -1;
     if (nthreads < 1) nthreads = 1;
     if (nthreads > 256) nthreads = 256;
     if (nthreads > n) nthreads = (int)n;
     mt_ctx c = {x, g, w, n, m, d, nthreads, l, tr, arith, idx, A, NULL, NULL};
+    c.gap = gap;
+    c.wv = wv;
+    c.rv = (double *)malloc(sizeof(double) * nthreads);
     c.bv = (double *)malloc(sizeof(double) * nthreads);
     c.bi = (int64_t *)malloc(sizeof(int64_t) * nthreads);
     pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * nthreads);
@@ -290,10 +314,106 @@ int sr_greedy_mt(const double *x, const double *g, const double *w, int64_t n, i
         for (int q = 1; q <= started; q++) pthread_join(th[q], NULL);
         pthread_barrier_destroy(&c.bar);
     }
+    free(c.rv);
     free(c.bv);
     free(c.bi);
     free(th);
     free(args);
+    return rc;
+}
+
+int sr_greedy_mt(const double *x, const double *g, const double *w, int64_t n, int d,
+                 double l, double tr, int64_t m, uint32_t *idx, double *A, int nthreads, int arith) {
+    return greedy_mt(x, g, w, n, d, l, tr, m, idx, A, nthreads, arith, NULL, NULL);
+}
+
+/*
+ * Near-tie guard of the compact arithmetic (the kernels' rule, persistent.hip tie_check): step t (the
+ * argmin that gives idx[t]) is flagged when the smallest running sum of any OTHER row -- an exact tie
+ * included -- lies within thr(t) of the winner's.  Exact ties count because the guard runs on problems
+ * without adjacent repeated rows (the drop-in thins the run starts, device.py dedup_view): two different
+ * rows with equal sums tie only by accident of rounding.  thr(t) bounds how far two rows' sums may move
+ * between the compact arithmetic, the exact one and NumPy's evaluation -- diagnostics.py's band (8 ulps
+ * per term of the magnitudes a pair value is built from, plus an ulp of the sum per step) for both rows,
+ * times 2 -- with ulp(v) <= |v| 2^-52 and the magnitudes bounded by
+ *   pair terms of row i against the column j:  scale <= (3 l + tr + sqrt(l) (gmax + |g_j|) + gmax |g_j|) wmax w_j
+ *     (3 l^2 S / qf^2.5 <= 3 l; l |sum dg delta| / qf^1.5 <= sqrt(l) |dg|; |g_i . g_j| / sqrt(qf) <= gmax |g_j|)
+ *     <= (c1 + |g_j|^2) wmax w_j,  c1 = 3 l + tr + sqrt(l) gmax + l / 2 + gmax^2 / 2   (a b <= (a^2 + b^2) / 2)
+ *   the diagonal:                               Dmax = (tr + gmax^2) wmax^2
+ *   a running sum at step s:                    |A_i(s)| <= Dmax + 2 sqrt(Dmax Q(s)) <= 2 Dmax + Q(s)
+ * where Q(s) = sum of the winners' sums before step s = the Stein quadratic form of the selected multiset
+ * (A_i(s) = |phi_i|^2 + 2 <phi_i, Phi_S>, Q = |Phi_S|^2: the kernel is positive semi-definite), gmax^2 =
+ * max_i |g_i|^2 and wmax^2 = max_i w_i^2 (1 without weights).  Recurrence (one lane per block of the
+ * kernels evaluates it with these operations in this order; no square root per step):
+ *   thr(0) = 2^-50 (8 Dmax);  for s >= 1 with j = idx[s-1], v = its sum at step s-1:
+ *     Q += v;  E += 16 (c1 + |g_j|^2) wmax w_j + (2 Dmax + max(Q, 0));  thr(s) = 2^-50 (8 Dmax + E)
+ */
+typedef struct {
+    double c1, wmax, dmax, Q, E, thr;
+} tie_state;
+
+static void tie_init(tie_state *ts, double l, double tr, double g2max, double w2max) {
+    const double gm = sqrt(g2max), sl = sqrt(l);
+    ts->c1 = (((3.0 * l + tr) + sl * gm) + 0.5 * l) + 0.5 * g2max;
+    ts->wmax = sqrt(w2max);
+    ts->dmax = (tr + g2max) * w2max;
+    ts->Q = 0.0;
+    ts->E = 0.0;
+    ts->thr = 0x1p-50 * (8.0 * ts->dmax);
+}
+
+/* one step: v = the previous winner's sum, gj its score row, wj its weight (1 without weights) */
+static void tie_step(tie_state *ts, double v, const double *gj, int d, double wj) {
+    ts->Q = ts->Q + v;
+    double gj2 = gj[0] * gj[0];
+    for (int k = 1; k < d; k++) gj2 = gj2 + gj[k] * gj[k];
+    const double scale = (ts->c1 + gj2) * (ts->wmax * wj);
+    ts->E = ts->E + (16.0 * scale + (2.0 * ts->dmax + fmax(ts->Q, 0.0)));
+    ts->thr = 0x1p-50 * (8.0 * ts->dmax + ts->E);
+}
+
+/* the bounds' inputs as the kernels compute them: max_i of g_i0 g_i0 + g_i1 g_i1 + ... (sequential) and of
+ * w_i w_i (1 without weights); a NaN counts as +inf */
+void sr_tie_bounds(const double *g, const double *w, int64_t n, int d, double *g2max, double *w2max) {
+    double gm = 0.0, wm = w ? 0.0 : 1.0;
+    for (int64_t i = 0; i < n; i++) {
+        double s = g[i * d] * g[i * d];
+        for (int k = 1; k < d; k++) s = s + g[i * d + k] * g[i * d + k];
+        if (isnan(s)) s = INFINITY;
+        gm = s > gm ? s : gm;
+        if (w) {
+            double v = w[i] * w[i];
+            if (isnan(v)) v = INFINITY;
+            wm = v > wm ? v : wm;
+        }
+    }
+    *g2max = gm;
+    *w2max = wm;
+}
+
+/* sr_greedy_mt plus the near-tie model per step: gap[t] = (smallest sum of any other row) - (the
+ * winner's) (NaN when a NaN won), thr[t] = the guard's threshold (recurrence above) and wv[t] = the
+ * winner's sum (wv may be NULL); the guard flags step t when gap[t] <= thr[t] */
+int sr_greedy_mt_ties(const double *x, const double *g, const double *w, int64_t n, int d,
+                      double l, double tr, int64_t m, uint32_t *idx, double *A, int nthreads, int arith,
+                      double *gap, double *thr, double *wv) {
+    double *v = wv ? wv : (double *)malloc(sizeof(double) * (m > 0 ? m : 1));
+    if (!v) return -2;
+    int rc = greedy_mt(x, g, w, n, d, l, tr, m, idx, A, nthreads, arith, gap, v);
+    if (rc == 0) {
+        double g2max, w2max;
+        sr_tie_bounds(g, w, n, d, &g2max, &w2max);
+        tie_state ts;
+        tie_init(&ts, l, tr, g2max, w2max);
+        for (int64_t t = 0; t < m; t++) {
+            if (t > 0) {
+                const int64_t j = idx[t - 1];
+                tie_step(&ts, v[t - 1], g + j * d, d, w ? w[j] : 1.0);
+            }
+            thr[t] = ts.thr;
+        }
+    }
+    if (!wv) free(v);
     return rc;
 }
 

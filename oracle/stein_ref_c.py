@@ -29,6 +29,11 @@ def lib():
         L.sr_greedy_mt.restype = ctypes.c_int
         L.sr_greedy_mt.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp, dp,
                                    ctypes.c_int, ctypes.c_int]
+        L.sr_greedy_mt_ties.restype = ctypes.c_int
+        L.sr_greedy_mt_ties.argtypes = [dp, dp, dp, i64, ctypes.c_int, ctypes.c_double, ctypes.c_double, i64, dp,
+                                        dp, ctypes.c_int, ctypes.c_int, dp, dp, dp]
+        L.sr_tie_bounds.restype = None
+        L.sr_tie_bounds.argtypes = [dp, dp, i64, ctypes.c_int, dp, dp]
         L.sr_pow_15_25.restype = None
         L.sr_pow_15_25.argtypes = [dp, i64, dp, dp]
         L.sr_pairs.restype = ctypes.c_int
@@ -85,6 +90,37 @@ def greedy_mt(x, g, w, l, tr, m, nthreads=None, arith=None):
                             _a(arith))
     assert rc == 0
     return idx, A
+
+
+def tie_bounds(g, w):
+    """(max_i |g_i|^2, max_i w_i^2) as the kernels compute them for the near-tie threshold."""
+    g = np.ascontiguousarray(g, dtype=np.float64)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    g2, w2 = ctypes.c_double(), ctypes.c_double()
+    lib().sr_tie_bounds(_p(g), _p(w), g.shape[0], g.shape[1], ctypes.byref(g2), ctypes.byref(w2))
+    return g2.value, w2.value
+
+
+def greedy_ties(x, g, w, l, tr, m, nthreads=None, arith=None, winner_sums=False):
+    """greedy_mt plus the kernels' near-tie guard model (stein_ref.c sr_greedy_mt_ties): (idx, A, gap, thr,
+    flagged) where gap[t] = the smallest running sum of any row other than the step-t winner minus the
+    winner's (exact ties count: 0), thr[t] the guard's threshold and flagged[t] = gap[t] <= thr[t] (only
+    with the compact arithmetic, d <= 8).  winner_sums=True appends wv[t], the step-t winner's sum."""
+    x = np.ascontiguousarray(x, dtype=np.float64)
+    g = np.ascontiguousarray(g, dtype=np.float64)
+    w = None if w is None else np.ascontiguousarray(w, dtype=np.float64)
+    n, d = x.shape
+    idx = np.empty(m, dtype=np.uint32)
+    A = np.empty(n, dtype=np.float64)
+    gap, thr, wv = (np.empty(m, dtype=np.float64) for _ in range(3))
+    rc = lib().sr_greedy_mt_ties(_p(x), _p(g), _p(w), n, d, l, tr, m, _p(idx), _p(A), nthreads or host_threads(),
+                                 _a(arith), _p(gap), _p(thr), _p(wv))
+    assert rc == 0
+    with np.errstate(invalid='ignore'):
+        flagged = (gap <= thr) & (_a(arith) == 1) & (d <= 8)
+    if winner_sums:
+        return idx, A, gap, thr, flagged, wv
+    return idx, A, gap, thr, flagged
 
 
 def pairs(x, g, w, l, tr, i1, i2, arith=None):

@@ -131,8 +131,9 @@ def test_greedy_concurrent_batches_by_d(monkeypatch):
 
 
 def test_thin_chains_raises_the_loops_error():
-    """thin_chains prepares the chains on host threads but raises what the loop of thin() calls
-    raises: the first failing chain's error (here chain 1's NaN, not chain 2's shape mismatch)."""
+    """thin_chains builds the chains one after the other and raises what the loop of thin() calls
+    raises: the first failing chain's error (here chain 1's NaN, not chain 2's shape mismatch); a bad
+    n_points after chain 0's input (the loop's first thin() checks it there); mismatched list lengths."""
     import re
     import stein_thinning
     rng = np.random.default_rng(9)
@@ -145,6 +146,19 @@ def test_thin_chains_raises_the_loops_error():
         [stein_thinning.thin(x, g, 10, preconditioner='med') for x, g in zip(xs, gs)]
     with pytest.raises(type(want.value), match=re.escape(str(want.value))):
         stein_thinning.thin_chains(xs, gs, 10, preconditioner='med')
+    for m in (0, -1):   # chain 0 valid, chain 1 NaN: the loop raises the n_points error first
+        with pytest.raises(Exception) as want:
+            [stein_thinning.thin(x, g, m, preconditioner='med') for x, g in zip(xs, gs)]
+        with pytest.raises(type(want.value), match=re.escape(str(want.value))):
+            stein_thinning.thin_chains(xs, gs, m, preconditioner='med')
+    gs0 = [-xs[0].copy()]
+    gs0[0][5, 1] = np.inf   # chain 0 invalid and n_points bad: the loop raises chain 0's input error
+    with pytest.raises(Exception) as want:
+        stein_thinning.thin(xs[0], gs0[0], 0, preconditioner='med')
+    with pytest.raises(type(want.value), match=re.escape(str(want.value))):
+        stein_thinning.thin_chains(xs[:1], gs0, 0, preconditioner='med')
+    with pytest.raises(ValueError, match='one entry per chain'):
+        stein_thinning.thin_chains(xs, gs[:2], 10)
     got = stein_thinning.thin_chains(xs[:1] + xs[3:], gs[:1] + gs[3:], 10, preconditioner='med')
     for x, g, idx in zip(xs[:1] + xs[3:], gs[:1] + gs[3:], got):
         np.testing.assert_array_equal(idx, stein_thinning.thin(x, g, 10, preconditioner='med'))

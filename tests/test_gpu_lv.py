@@ -144,3 +144,18 @@ def test_phase_b_pieces_per_lane(data, pieces):
     assert err.max() < 1e-11, err.max()
     ref = np.stack([ol.grad_log_posterior(t, data.t, data.y, data.cov) for t in th[:12]])
     assert (np.abs(got[:12] - ref) / np.abs(ref).max(axis=1, keepdims=True)).max() < RTOL
+
+
+@pytest.mark.parametrize('t_n', [2643, 2644, 2700, 2731, 4000])
+def test_phase_b_observation_count_at_the_lds_boundary(data, t_n):
+    """Phase B stages the observations in LDS when 3 t_n doubles fit next to its static LDS in 64 KB
+    (t_n <= 2643), else reads them from global memory (the static part is counted); either
+    side of the boundary agrees with the single-phase kernel."""
+    t = np.linspace(0.0, 25.0, t_n)
+    y = np.stack([np.interp(t, data.t, data.y[:, 0]), np.interp(t, data.t, data.y[:, 1])], axis=1)
+    custom = lv.LvData(t=t, y=y)
+    th = _points(24, 0.05, 11)
+    got = lv.grad_log_posterior(th, custom)
+    want = _single_phase(th, custom)
+    err = np.abs(got - want) / np.abs(want).max(axis=1, keepdims=True)
+    assert err.max() < 1e-11, err.max()

@@ -1,0 +1,144 @@
+"""Near-tie guard on the GPU: the persistent kernel's flag equals the bit model's
+(oracle/stein_ref.c sr_greedy_mt_ties) -- the first flagged step, the bounds and the final threshold
+state bit for bit -- and the drop-in thin with default settings returns the NumPy path's indices on the
+near-tie construction where the compact arithmetic alone departs from them (tests/test_gpu_margins.py)."""
+import numpy as np
+import pytest
+
+from oracle import stein_numpy as o
+from oracle import stein_ref_c as oc
+from tests import margins_ref as mr
+from tests.test_near_tie_cpu import model_thresholds
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip('torch')
+if not torch.cuda.is_available():
+    pytest.skip('no HIP device', allow_module_level=True)
+
+import stein_thinning  # noqa: E402
+from stein_thinning import _native as nat  # noqa: E402
+from stein_thinning import device as dv  # noqa: E402
+from stein_thinning import thinning as st  # noqa: E402
+
+BOUNDS = 1088 // 8   # csrc/stein_internal.hpp kWsBoundsOff: max |g|^2, max w^2, then the final Q, E, thr
+
+
+def _compact_run(prob, m):
+    """One st_greedy (compact arithmetic, guard on) on the problem as it is: (indices, first flagged step,
+    [g2max, w2max, Q, E, thr] the kernel left in the workspace)."""
+    idx, a, ws = prob.greedy_buffers(m)
+    prob.greedy_launch(m, idx, a, ws)
+    out = idx.cpu().numpy().view(np.uint32).copy()
+    step = nat.near_tie_step(ws)
+    return out, step, ws[BOUNDS:BOUNDS + 5].cpu().numpy()
+
+
+@pytest.mark.parametrize('seed', range(10))
+def test_kernel_flag_and_state_equal_bit_model(seed):
+    X, G, steps = mr.near_tie_twins(seed)
+    integrand = st._make_stein_integrand(X, G)
+    prob = integrand.device_problem()
+    idx, step, state = _compact_run(prob, 30)
+    midx, _, gap, thr, flagged, wv = oc.greedy_ties(integrand.sample, integrand.gradient, None,
+                                                    integrand.linv_scale, integrand.linv_trace, 30,
+                                                    winner_sums=True)
+    np.testing.assert_array_equal(idx, midx)
+    assert step == steps[0] == np.flatnonzero(flagged)[0]
+    g2, w2 = oc.tie_bounds(integrand.gradient, None)
+    thr_all, Q, E = model_thresholds(integrand.gradient, None, integrand.linv_scale, integrand.linv_trace, midx, wv)
+    np.testing.assert_array_equal(state, [g2, w2, Q, E, thr_all[-1]])
+
+
+def test_kernel_state_gradient_free_and_unflagged():
+    from oracle import models
+    sample, gradient, log_p, _, _ = models.bivariate_reference_sample(1000)
+    log_q, gq, _, _ = models.gaussian_proxy(sample, 2)
+    integrand = st._make_stein_gf_integrand(sample, log_p, log_q, gq, preconditioner='med')
+    idx, step, state = _compact_run(integrand.device_problem(), 200)
+    midx, _, _, _, flagged, wv = oc.greedy_ties(integrand.sample, integrand.gradient, integrand.weights,
+                                                integrand.linv_scale, integrand.linv_trace, 200, winner_sums=True)
+    np.testing.assert_array_equal(idx, midx)
+    assert step == -1 and not flagged.any()
+    thr_all, Q, E = model_thresholds(integrand.gradient, integrand.weights, integrand.linv_scale,
+                                     integrand.linv_trace, midx, wv)
+    np.testing.assert_array_equal(state, list(oc.tie_bounds(integrand.gradient, integrand.weights)) +
+                                  [Q, E, thr_all[-1]])
+
+
+@pytest.mark.parametrize('seed', range(10))
+def test_dropin_thin_equals_numpy_on_near_ties(seed):
+    X, G, steps = mr.near_tie_twins(seed)
+    integrand = st._make_stein_integrand(X, G)
+    got = st._greedy_search(30, integrand)
+    np.testing.assert_array_equal(got, o.thin(X, G, 30))
+    prob = integrand.device_problem()
+    assert prob.near_tie == steps[0]   # flagged, re-run with the exact arithmetic
+    np.testing.assert_array_equal(stein_thinning.thin(X, G, 30), o.thin(X, G, 30))
+
+
+def test_guard_off_keeps_the_compact_selection():
+    X, G, _ = mr.near_tie_twins(0)
+    want = o.thin(X, G, 30)
+    nat.set_near_tie_guard(False)
+    try:
+        integrand = st._make_stein_integrand(X, G)
+        got = st._greedy_search(30, integrand)
+        assert integrand.device_problem().near_tie is None
+        idx, step, _ = _compact_run(integrand.device_problem(), 30)
+        assert step == -2   # the kernel computed no flag
+    finally:
+        nat.set_near_tie_guard(None)
+    assert not np.array_equal(got, want)   # seed 0: the compact arithmetic alone departs at step 8
+
+
+def test_exact_arithmetic_needs_no_guard():
+    X, G, _ = mr.near_tie_twins(1)
+    with nat.arithmetic_override('exact'):
+        integrand = st._make_stein_integrand(X, G)
+        prob = integrand.device_problem()
+        assert prob.guard_mode() is None
+        np.testing.assert_array_equal(st._greedy_search(30, integrand), o.thin(X, G, 30))
+        assert _compact_run(prob, 30)[1] == -2
+
+
+@pytest.mark.parametrize('d', [1, 3, 5, 8])
+def test_other_d_run_exact(d):
+    """d outside {2, 4}: the launch-per-step kernels carry no flag, so the guarded drop-in runs them in the
+    exact arithmetic: NumPy's indices, near-tie twins included."""
+    rng = np.random.default_rng(d)
+    X = rng.normal(size=(300, d))
+    G = -X
+    pick = o.thin(X, G, 12)[8:12]
+    Xt = X[pick].copy()
+    for _ in range(4):
+        Xt[:, 0] = np.nextafter(Xt[:, 0], np.inf)
+    X2, G2 = np.vstack([X, Xt]), np.vstack([G, G[pick]])
+    integrand = st._make_stein_integrand(X2, G2)
+    assert integrand.device_problem().guard_mode() == 'exact'
+    np.testing.assert_array_equal(st._greedy_search(25, integrand), o.thin(X2, G2, 25))
+
+
+def test_thin_chains_guarded():
+    """thin_chains (one batch launch): each chain's tie word is read, flagged chains re-run exactly."""
+    problems = [mr.near_tie_twins(s)[:2] for s in range(3)]
+    rng = np.random.default_rng(5)
+    Z = rng.normal(size=(405, 2))
+    problems.append((Z, -Z))
+    got = stein_thinning.thin_chains([p[0] for p in problems], [p[1] for p in problems], 30)
+    for (X, G), idx in zip(problems, got):
+        np.testing.assert_array_equal(idx, o.thin(X, G, 30))
+
+
+def test_config2_run_starts_unflagged():
+    """Config 2 through the drop-in path: the run starts are thinned (the guard counts exact ties), no step
+    is flagged, and the indices equal the plain full thin's."""
+    import bench
+    cfg = dict(bench.CONFIGS['c2'])
+    integrand, _, _ = bench.make_integrand(cfg)
+    prob = integrand.device_problem()
+    got = prob.greedy(cfg["m"], dedup=True, guard=True)
+    assert prob.dedup_used and prob.near_tie == -1
+    full, _ = oc.greedy_mt(integrand.sample, integrand.gradient, None, integrand.linv_scale, integrand.linv_trace,
+                           cfg['m'])
+    np.testing.assert_array_equal(got, full)
