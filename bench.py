@@ -392,6 +392,9 @@ def main():
     ap.add_argument('--energy-variant', type=int, default=0, help='energy kernel (st_tune key 13; 0 = auto)')
     ap.add_argument('--energy-units', type=int, default=-1,
                     help='energy kernel work units per launch (st_tune key 14; -1 = auto)')
+    ap.add_argument('--headline-guard', action='store_true',
+                    help='thin workload: time the headline thin with the near-tie guard on (default off: the guard is '
+                         'timed beside it, "near_tie_guard")')
     ap.add_argument('--arith', default='compact', choices=['compact', 'exact'],
                     help='arithmetic of the d <= 8 greedy kernels (stein_thinning.set_arithmetic)')
     ap.add_argument('--chains', type=int, default=5,
@@ -448,6 +451,11 @@ def main():
     import stein_thinning
     stein_thinning.set_arithmetic(args.arith)
     arithmetic = args.arith
+    from stein_thinning import _native as nat
+    # the headline leg: st_greedy over all n rows as the kernel computes them (compact arithmetic: no
+    # near-tie flag, unless --headline-guard).  The drop-in thin's default (guard on) is timed beside it:
+    # "near_tie_guard" (all rows) and "dedup" (the run starts, the drop-in's path on repeated rows).
+    nat.set_near_tie_guard(bool(args.headline_guard))
 
     if not sharded:
         prob = integrand.device_problem()
@@ -599,6 +607,29 @@ def main():
                 stein_thinning.set_arithmetic('compact')
                 run_once()   # leave the buffers as the timed (compact) run left them
                 torch.cuda.synchronize()
+        guarded = None
+        nat.set_near_tie_guard(None)   # the drop-in default from here on (ST_NEAR_TIE, on unless '0')
+        if world == 1 and not sharded and d in (2, 4) and arithmetic == 'compact' and nat.near_tie_guard():
+            # the same thin of all n rows with the near-tie guard (not `value`): its time and first
+            # flagged step (-1 none; rows that repeat their predecessor tie exactly, so a raw MCMC sample
+            # is flagged at once -- the drop-in thins its run starts instead, "dedup")
+            run_once()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(3)]
+            for e0, e1 in ev:
+                e0.record(stream)
+                run_once()
+                e1.record(stream)
+            torch.cuda.synchronize()
+            try:
+                tie = nat.near_tie_step(ws)
+            except nat.HipExtensionError:   # an older A/B build (ST_HIP_LIB) without the guard
+                tie = None
+            guarded = {'ms_per_thin': round(float(np.median([a.elapsed_time(b) for a, b in ev])), 4),
+                       'first_flagged_step': tie,
+                       'same_indices_as_timed_run': bool(np.array_equal(idx.cpu().numpy().view(np.uint32),
+                                                                        result_idx)),
+                       'note': 'st_greedy of all n rows with the near-tie guard (DESIGN.md section 1); a flagged '
+                               'drop-in thin is re-run in the exact arithmetic ("exact_arithmetic")'}
         dedup = None
         if world == 1 and not sharded:
             dedup = dedup_timing(prob, m, result_idx, stream)
@@ -617,6 +648,21 @@ def main():
             e2e = {'thin_host_arrays_s': round(dt_e, 4), 'runs_s': [round(v, 4) for v in dts],
                    'pair_evals_per_s': n * m / dt_e,
                    'same_indices_as_timed_run': bool(np.array_equal(e2e_idx, result_idx))}
+            # the same call on ROCm tensors already on the GPU (the raw sample and gradient, row-major):
+            # x comes down for its statistics and the 'med' subsample, g stays (thinning._download_standardized)
+            xd = torch.from_numpy(np.ascontiguousarray(host_x)).to(dev)
+            gd = torch.from_numpy(np.ascontiguousarray(host_g)).to(dev)
+            torch.cuda.synchronize()
+            st.thin(xd, gd, m, preconditioner='med')
+            dts = []
+            for _ in range(3):
+                t_e = time.perf_counter()
+                dev_idx = st.thin(xd, gd, m, preconditioner='med')
+                dts.append(time.perf_counter() - t_e)
+            e2e['thin_device_tensors_s'] = round(float(np.median(dts)), 4)
+            e2e['device_tensors_runs_s'] = [round(v, 4) for v in dts]
+            e2e['device_tensors_same_indices'] = bool(np.array_equal(dev_idx, result_idx))
+            del xd, gd
 
     exchange, degraded = None, False
     if sharded:
@@ -651,6 +697,8 @@ def main():
                        'parallelism': (f'rows-sharded x{world}, per-step exchange: {runner.mode}'
                                        if sharded else 'single-gpu'),
                        'arithmetic': arithmetic if d <= 8 else 'exact',
+                       'near_tie_guard': bool(args.headline_guard and d in (2, 4) and arithmetic == 'compact'
+                                              and not sharded),
                        'wallclock_thin_s': {
                            'device_resident': elapsed / args.steps,
                            'device_resident_dedup': (round(dedup['s_per_thin_incl_detect'], 6)
@@ -670,6 +718,7 @@ def main():
             'cpu_baseline': cpu,
             'end_to_end': e2e if rank == 0 and not sharded else None,
             'exact_arithmetic': exact if rank == 0 and not sharded else None,
+            'near_tie_guard': guarded if rank == 0 and not sharded else None,
             'dedup': dedup if rank == 0 and not sharded else None,
         }
         print(json.dumps(line), flush=True)

@@ -116,9 +116,64 @@ StatsFn stats_for(int d) {
     }
 }
 
+// loc / scl of a NaN / inf-free x outside the d = 2 .. 8 single pass: d == 1 the pairwise column sum,
+// d > 8 row-by-row accumulation (NumPy's axis-0 order: sequential per column) with the columns split
+// over up to hw threads (contiguous column groups)
+template <typename Par>
+void stats_general(const double* sample, int64_t n, int d, int hw, double* loc, double* scl, Par&& parallel) {
+    const double dn = (double)n;
+    if (d == 1) {
+        loc[0] = numpy_column_sum(sample, n) / dn;
+        std::vector<double> dev((size_t)n);
+        for (int64_t i = 0; i < n; ++i) dev[i] = fabs(sample[i] - loc[0]);
+        scl[0] = numpy_column_sum(dev.data(), n) / dn;
+        return;
+    }
+    const int tc = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)hw, (int64_t)d, n / 65536}));
+    parallel(tc, [&](int t, int T) {
+        const int j0 = d * t / T, j1 = d * (t + 1) / T, w = j1 - j0;
+        std::vector<double> acc(sample + j0, sample + j1);
+        for (int64_t i = 1; i < n; ++i) {
+            const double* row = sample + i * d + j0;
+            for (int j = 0; j < w; ++j) acc[j] += row[j];
+        }
+        for (int j = 0; j < w; ++j) loc[j0 + j] = acc[j] / dn;
+        for (int j = 0; j < w; ++j) acc[j] = fabs(sample[j0 + j] - loc[j0 + j]);
+        for (int64_t i = 1; i < n; ++i) {
+            const double* row = sample + i * d + j0;
+            for (int j = 0; j < w; ++j) acc[j] += fabs(row[j] - loc[j0 + j]);
+        }
+        for (int j = 0; j < w; ++j) scl[j0 + j] = acc[j] / dn;
+    });
+}
+
+// run fn(t, T) on T threads (T = 1: inline)
+struct Parallel {
+    template <typename Fn>
+    void operator()(int T, Fn&& fn) const {
+        if (T <= 1) { fn(0, 1); return; }
+        std::vector<std::thread> th;
+        for (int t = 0; t < T; ++t) th.emplace_back([&fn, t, T] { fn(t, T); });
+        for (auto& x : th) x.join();
+    }
+};
+
 }  // namespace
 
 namespace st {
+// for st_standardize_download (prep_upload.cpp): x's NaN / inf flags, then loc / scl, any n >= 1, d >= 1
+void column_stats_any(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf) {
+    if (StatsFn f = stats_for(d)) { f(x, n, loc, scl, nan, inf); return; }
+    int fn = 0, fi = 0;
+    for (int64_t e = 0; e < n * (int64_t)d; ++e) {
+        fn |= (int)(x[e] != x[e]);
+        fi |= (int)(fabs(x[e]) == INFINITY);
+    }
+    nan = fn;
+    inf = fi;
+    if (fn | fi) return;
+    stats_general(x, n, d, hardware_threads(), loc, scl, Parallel{});
+}
 // for st_standardize_upload (prep_upload.cpp): the d = 2 .. 8 single-thread column pass over x
 bool column_stats_fast(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf) {
     StatsFn f = stats_for(d);
@@ -139,15 +194,8 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
     *status = 0;
     const int64_t total = n * (int64_t)d;
     const int hw = hardware_threads();
-    // run fn(t, T) on T threads (T = 1: inline)
-    auto parallel = [](int T, auto&& fn) {
-        if (T <= 1) { fn(0, 1); return; }
-        std::vector<std::thread> th;
-        for (int t = 0; t < T; ++t) th.emplace_back([&fn, t, T] { fn(t, T); });
-        for (auto& x : th) x.join();
-    };
+    const Parallel parallel;
     std::vector<double> loc(d, 0.0), scl(d, 0.0);
-    const double dn = (double)n;
     StatsFn fast = standardize && n >= 65536 ? stats_for(d) : nullptr;
     if (fast) {
         // thread 0: x's flags, column sums and absolute deviations; the others: g's flags
@@ -190,33 +238,7 @@ extern "C" int st_standardize_host(const double* sample, const double* gradient,
         if (gradient_out != gradient) memcpy(gradient_out, gradient, (size_t)total * 8);
         return ST_OK;
     }
-    if (fast) {
-        // loc, scl done above
-    } else if (d == 1) {
-        loc[0] = numpy_column_sum(sample, n) / dn;
-        std::vector<double> dev((size_t)n);
-        for (int64_t i = 0; i < n; ++i) dev[i] = fabs(sample[i] - loc[0]);
-        scl[0] = numpy_column_sum(dev.data(), n) / dn;
-    } else {
-        // row-by-row accumulation acc[j] += x[i, j] (NumPy's axis-0 reduction order): sequential
-        // per column, so the columns are split over threads (contiguous column groups)
-        const int tc = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)hw, (int64_t)d, n / 65536}));
-        parallel(tc, [&](int t, int T) {
-            const int j0 = d * t / T, j1 = d * (t + 1) / T, w = j1 - j0;
-            std::vector<double> acc(sample + j0, sample + j1);
-            for (int64_t i = 1; i < n; ++i) {
-                const double* row = sample + i * d + j0;
-                for (int j = 0; j < w; ++j) acc[j] += row[j];
-            }
-            for (int j = 0; j < w; ++j) loc[j0 + j] = acc[j] / dn;
-            for (int j = 0; j < w; ++j) acc[j] = fabs(sample[j0 + j] - loc[j0 + j]);
-            for (int64_t i = 1; i < n; ++i) {
-                const double* row = sample + i * d + j0;
-                for (int j = 0; j < w; ++j) acc[j] += fabs(row[j] - loc[j0 + j]);
-            }
-            for (int j = 0; j < w; ++j) scl[j0 + j] = acc[j] / dn;
-        });
-    }
+    if (!fast) stats_general(sample, n, d, hw, loc.data(), scl.data(), parallel);   // else: done above
     for (int j = 0; j < d; ++j)
         if (scl[j] == 0.0) { *status = 3; return ST_OK; }
     if (loc_out) memcpy(loc_out, loc.data(), (size_t)d * 8);

@@ -147,7 +147,7 @@ int persistent_tune(int key, int value) {
         return 0;
     }
     if (key == 21) {
-        if (value < 0 || value > 31) return -1;
+        if (value < 0 || value > 63) return -1;
         g_tie_dbg = value;
         return 0;
     }

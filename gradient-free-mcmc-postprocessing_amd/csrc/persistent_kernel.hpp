@@ -71,7 +71,11 @@ struct GuardScratch {
     double win_v[2], blk_v[2];
     double win_row[2][kMaxCtDim + 1];
     double tg[6];         // recurrence state (stein_ref.c tie_state): c1, wmax, Dmax, Q, E, thr
-    double bnd[2];        // the block's max_i |g_i|^2, max_i w_i^2 (staging)
+    double bnd[kMaxPWaves][2];   // per wave: max_i |g_i|^2, max_i w_i^2 over its rows (staging)
+    // 512-thread kernels: wave 0's per-lane rescan of its register rows (step t - 1, written at the start
+    // of step t), reduced by wave 1 after publishing step t, off the critical path
+    double w0_b[64], w0_b2[64];
+    uint32_t w0_bi[64];
     int tied;             // a step was flagged (this block's word was written)
 };
 
@@ -228,7 +232,8 @@ struct PersistArgs {
     const double* tie_bounds;
     unsigned* tie;
     int tie_dbg;          // st_tune key 21 (measurement only): 1 skip the waves' rescans, 2 skip the check,
-                          // 4 skip wave 0's rescan (the guard's verdict is then meaningless)
+                          // 4 skip wave 0's rescan, 8 / 16 the streamed / LDS rows', 32 the bounds pass
+                          // (the guard's verdict is then meaningless)
 };
 
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
@@ -389,8 +394,10 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 // rule, the bound thr(t) and its recurrence).  Nothing is added to the pair loop or to the exchange's
 // critical path: after publishing step t the waves that do not sweep rescan the block's running sums
 // (already on chip: registers, LDS, and the streamed rows' sums in L2) for the minimum, its row and the
-// second-smallest sum per wave, and the sweeping wave rescans its own register rows while its first
-// poll is in flight.  One step later (during step t + 1's exchange) one lane checks step t: in the
+// second-smallest sum per wave; the picking wave (wave 0) rescans its own register rows while its first
+// poll is in flight (512-thread kernels: right after the pick) and leaves one (minimum, row,
+// second-smallest) per lane in LDS, which wave 1 reduces after the next publish.  One step later
+// (during step t + 1's exchange) one lane checks step t: in the
 // winner's block, the block's second-smallest sum against the winner's; in every other block, the
 // block's minimum against it -- together exactly the model's rule -- and a flagged block writes ~t into
 // the tie word with an atomic max (the largest ~t = the first flagged step).  The same lane advances
@@ -433,13 +440,13 @@ __device__ __forceinline__ double wave_min_f64(double m) {
 }
 
 // the calling wave's (minimum, its row, second-smallest) into slot [par][wave]; every lane active
-__device__ __forceinline__ void top2_wave(GuardScratch* sc, const Top2& r, int par) {
+__device__ __forceinline__ void top2_wave(GuardScratch* sc, const Top2& r, int par, int w = -1) {
     double v = r.b;
     int64_t i = r.bi == 0xFFFFFFFFu ? INT64_MAX : (int64_t)r.bi;
     p_wave_minloc(v, i);
     const double c = wave_min_f64((r.bi != 0xFFFFFFFFu && (int64_t)r.bi == i) ? r.b2 : r.b);
     if ((threadIdx.x & 63) == 0) {
-        const int w = threadIdx.x >> 6;
+        if (w < 0) w = threadIdx.x >> 6;
         sc->rs_min[par][w] = v;
         sc->rs_idx[par][w] = i == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)i;
         sc->rs_run[par][w] = c;
@@ -948,7 +955,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         // g_i0 g_i0 + g_i1 g_i1 + ... and of w_i w_i over this block's rows, a NaN as +inf, merged into the
         // problem's words with u64 atomic maxima that complete before any record of this block is
         // published (the fence) -- so a block that has seen every step-0 record sees the final bounds
-        if (guard) {
+        if (guard && !(a.tie_dbg & 32)) {
             double gm = 0.0, wm = GF ? 0.0 : 1.0;
             auto take_row = [&](double s2, double wv) {
                 gm = __builtin_fmax(gm, __builtin_isnan(s2) ? INFINITY : s2);
@@ -980,17 +987,29 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             gm = wave_max_f64(gm);
             wm = wave_max_f64(wm);
             if ((tid & 63) == 0) {
-                uint64_t* bw = reinterpret_cast<uint64_t*>(const_cast<double*>(a.tie_bounds));
-                __hip_atomic_fetch_max(bw, (uint64_t)__double_as_longlong(gm), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                __hip_atomic_fetch_max(bw + 1, (uint64_t)__double_as_longlong(wm), __ATOMIC_RELAXED,
-                                       __HIP_MEMORY_SCOPE_AGENT);
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+                gsc->bnd[tid >> 6][0] = gm;
+                gsc->bnd[tid >> 6][1] = wm;
             }
         }
     }
     if (tid == 0) { sc->ctr[0] = 0; sc->ctr[1] = 0; }
     const int block_fast = __syncthreads_and(rok);
+    if constexpr (GUARD && !kWide) {
+        // one atomic pair per block; their latency overlaps step 0's diagonal, and the release fence
+        // in front of publish(0) orders them before this block's step-0 record (written by wave 0)
+        if (guard && tid == 0 && !(a.tie_dbg & 32)) {
+            double gm = gsc->bnd[0][0], wm = gsc->bnd[0][1];
+            for (int w = 1; w < NT / 64; ++w) {
+                gm = __builtin_fmax(gm, gsc->bnd[w][0]);
+                wm = __builtin_fmax(wm, gsc->bnd[w][1]);
+            }
+            uint64_t* bw = reinterpret_cast<uint64_t*>(const_cast<double*>(a.tie_bounds));
+            __hip_atomic_fetch_max(bw, (uint64_t)__double_as_longlong(gm), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            __hip_atomic_fetch_max(bw + 1, (uint64_t)__double_as_longlong(wm), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+        }
+    }
 
     // ---- step 0: diagonal --------------------------------------------------------------------
     // running best of this thread: starts at its first row (register row 0, which precedes all its
@@ -1038,6 +1057,9 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             scan_take(kv, (uint32_t)row, bv, bi);
         }
     }
+    if constexpr (GUARD) {
+        if (guard && tid < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the bounds (above)
+    }
     publish<NT, GUARD>(a, sc, bv, bi, 0, r1, bid(), gsc);
 
     // near-tie guard: the rescans of the block's running sums after each publish (module comment above
@@ -1065,6 +1087,21 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         }
         top2_wave(gsc, r, (int)(tt & 1));
     };
+    // wave 0's own rescan leaves one Top2 per lane in LDS; wave 1 reduces them after the next publish
+    auto rescan_w0 = [&]() {
+        Top2 r;
+        rescan_regs(r);
+        gsc->w0_b[tid] = r.b;
+        gsc->w0_b2[tid] = r.b2;
+        gsc->w0_bi[tid] = r.bi;
+    };
+    auto reduce_w0 = [&](int64_t tt) {   // wave 1
+        Top2 r;
+        r.b = gsc->w0_b[tid - 64];
+        r.b2 = gsc->w0_b2[tid - 64];
+        r.bi = gsc->w0_bi[tid - 64];
+        top2_wave(gsc, r, (int)(tt & 1), 0);
+    };
     if constexpr (GUARD) {
         if (guard && tid >= 64 && !(a.tie_dbg & 1)) rescan_rest(0);
     }
@@ -1073,18 +1110,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     int64_t t = 1;
     for (; t < a.m; ++t) {
         const int64_t win = wait_and_pick<D, GF, kMaxG, GUARD>(a, sc, t - 1, bid(), G(), gsc, guard,
-                                                               guard && !kDyn && !(a.tie_dbg & 4), [&]() {
-            Top2 r;
-            rescan_regs(r);
-            top2_wave(gsc, r, (int)((t - 1) & 1));
-        });
+                                                               guard && !kDyn && !(a.tie_dbg & 4), rescan_w0);
         if (win < 0) break;
-        if constexpr (GUARD && kDyn) {   // wave 0's register rows of step t - 1 (the dynamic chunks absorb it)
-            if (guard && tid < 64 && !(a.tie_dbg & 4)) {
-                Top2 r;
-                rescan_regs(r);
-                top2_wave(gsc, r, (int)((t - 1) & 1));
-            }
+        if constexpr (GUARD && kDyn) {   // wave 0's register rows of step t - 1: per lane into LDS (wave 1
+            if (guard && tid < 64 && !(a.tie_dbg & 4)) rescan_w0();   // reduces them after publish(t))
         }
         if (bid() == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
         // chunk counter of the NEXT step (its last use, step t - 1, ended before publish's barrier)
@@ -1381,6 +1410,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         ST_STAMP(a, t, 4);
         if constexpr (GUARD) {
             if (guard && tid >= 64) {   // off the critical path: these waves only wait for the sweep now
+                if (tid < 128 && !(a.tie_dbg & 4)) reduce_w0(t - 1);   // wave 0's lanes of step t - 1
                 if (tid == 64 && !(a.tie_dbg & 2)) tie_check<D, GF>(a, gsc, t - 1, r0, r1, kNW);
                 if (!(a.tie_dbg & 1)) rescan_rest(t);
             }
@@ -1389,11 +1419,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     int64_t done = t;   // idx[0 .. done-1) are written
     if (t == a.m) {
         const int64_t win = wait_and_pick<D, GF, kMaxG, GUARD>(a, sc, a.m - 1, bid(), G(), gsc, guard,
-                                                               guard && !kDyn, [&]() {
-            Top2 r;
-            rescan_regs(r);
-            top2_wave(gsc, r, (int)((a.m - 1) & 1));
-        });
+                                                               guard && !kDyn, rescan_w0);
         if (win >= 0) {
             if (bid() == 0 && tid == 0) a.idx_out[a.m - 1] = (uint32_t)win;
             done = a.m + 1;
@@ -1401,13 +1427,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     }
     if constexpr (GUARD) {
         if (kDyn && guard && done == a.m + 1) {
-            if (tid < 64) {
-                Top2 r;
-                rescan_regs(r);
-                top2_wave(gsc, r, (int)((a.m - 1) & 1));
-            }
+            if (tid < 64) rescan_w0();
             __syncthreads();
         }
+        if (guard && tid >= 64 && tid < 128 && done == a.m + 1) reduce_w0(a.m - 1);
         if (guard && tid == 64 && done == a.m + 1) {
             tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW);
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)

@@ -26,6 +26,7 @@
 
 namespace st {
 bool column_stats_fast(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf);
+void column_stats_any(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf);
 int host_threads();
 int report_error(int code, const char* msg);   // capi.hip: sets st_last_error()
 }  // namespace st
@@ -130,6 +131,58 @@ extern "C" int st_standardize_upload(const double* sample, const double* gradien
     return ST_OK;
 }
 
+namespace {
+// st_standardize_download's two column passes over the page-locked copy, the first one chunk by chunk
+// as the copies land (event c = rows [c kRows, (c + 1) kRows) are on the host): the sequential sums of
+// st_standardize_host's column_stats, x's NaN / inf flags, then the absolute deviations from loc
+template <int D>
+int download_stats(const double* x, int64_t n, int64_t kRows, const std::vector<hipEvent_t>& ev, double* loc,
+                   double* scl, int& nan, int& inf) {
+    double acc[D];
+    int fn = 0, fi = 0;
+    for (size_t c = 0; c < ev.size(); ++c) {
+        if (hipEventSynchronize(ev[c]) != hipSuccess) return ST_ERR_HIP;
+        const int64_t r0 = (int64_t)c * kRows, r1 = std::min(n, r0 + kRows);
+        int64_t i = r0;
+        if (c == 0) {
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                acc[j] = x[j];
+                fn |= (int)(x[j] != x[j]);
+                fi |= (int)(fabs(x[j]) == INFINITY);
+            }
+            i = 1;
+        }
+        for (; i < r1; ++i) {
+            const double* row = x + i * D;
+            __builtin_prefetch(row + 64 * D);
+#pragma unroll
+            for (int j = 0; j < D; ++j) {
+                acc[j] += row[j];
+                fn |= (int)(row[j] != row[j]);
+                fi |= (int)(fabs(row[j]) == INFINITY);
+            }
+        }
+    }
+    nan = fn;
+    inf = fi;
+    if (fn | fi) return ST_OK;
+    const double dn = (double)n;
+    double l[D];
+#pragma unroll
+    for (int j = 0; j < D; ++j) { l[j] = acc[j] / dn; acc[j] = fabs(x[j] - l[j]); }
+    for (int64_t i = 1; i < n; ++i) {
+        const double* row = x + i * D;
+        __builtin_prefetch(row + 64 * D);
+#pragma unroll
+        for (int j = 0; j < D; ++j) acc[j] += fabs(row[j] - l[j]);
+    }
+#pragma unroll
+    for (int j = 0; j < D; ++j) { loc[j] = l[j]; scl[j] = acc[j] / dn; }
+    return ST_OK;
+}
+}  // namespace
+
 // The reverse direction for samples that already live on the device (the drop-in thin called with ROCm
 // tensors): only x has to visit the host -- the column sums are one dependency chain of n adds per
 // column, which a CPU core runs ~8x faster than a GPU lane -- and g never leaves the device (its NaN /
@@ -137,15 +190,33 @@ extern "C" int st_standardize_upload(const double* sample, const double* gradien
 // summed as it lands (NumPy's axis-0 order: acc[j] += x[i, j], row after row), then the absolute
 // deviations from loc in a second pass over the page-locked copy; the caller scales on the device
 // (st_layout_soa_scaled from the original device arrays).  *status: 0 ok, 1 NaN in x, 2 inf in x, 3 a
-// zero scale (x's flags only).  d = 2 .. 8 and n >= 65536 only (ST_ERR_UNSUPPORTED otherwise).
+// zero scale (x's flags only).  Other shapes (d = 1 or d > 8, n < 65536): one copy, then the host
+// routine's column passes (d = 1: NumPy's pairwise sums over its default 8192-element buffer).
 extern "C" int st_standardize_download(const double* dev_x, int64_t n, int32_t d, double* stage_x, double* loc_out,
                                        double* scl_out, int32_t* status, void* stream) {
     if (!dev_x || !stage_x || !loc_out || !scl_out || !status)
         return st::report_error(ST_ERR_INVALID, "st_standardize_download: NULL pointer");
-    if (d < 2 || d > 8 || n < 65536)
-        return st::report_error(ST_ERR_UNSUPPORTED, "st_standardize_download: d = 2 .. 8 and n >= 65536 only");
+    if (n < 1 || d < 1) return st::report_error(ST_ERR_INVALID, "st_standardize_download: empty input");
     *status = 0;
     hipStream_t s = static_cast<hipStream_t>(stream);
+    if (d < 2 || d > 8 || n < 65536) {   // one copy, then the host routine's column passes on x alone
+        if (hipMemcpyAsync(stage_x, dev_x, (size_t)n * d * 8, hipMemcpyDeviceToHost, s) != hipSuccess ||
+            hipStreamSynchronize(s) != hipSuccess)
+            return st::report_error(ST_ERR_HIP, "st_standardize_download: a device-to-host copy failed");
+        std::vector<double> l((size_t)d), c((size_t)d);
+        int fn = 0, fi = 0;
+        st::column_stats_any(stage_x, n, d, l.data(), c.data(), fn, fi);
+        if (fn || fi) {
+            *status = fn ? 1 : 2;
+            return ST_OK;
+        }
+        for (int j = 0; j < d; ++j) {
+            if (c[j] == 0.0) *status = 3;
+            loc_out[j] = l[j];
+            scl_out[j] = c[j];
+        }
+        return ST_OK;
+    }
     constexpr int64_t kRows = 1 << 16;
     const int64_t chunks = (n + kRows - 1) / kRows;
     std::vector<hipEvent_t> ev((size_t)chunks, nullptr);
@@ -158,18 +229,16 @@ extern "C" int st_standardize_download(const double* dev_x, int64_t n, int32_t d
             hipEventRecord(ev[c], s) != hipSuccess)
             rc = ST_ERR_HIP;
     }
-    double acc[8], l[8];
     int fn = 0, fi = 0;
-    for (int64_t c = 0; c < chunks && rc == ST_OK; ++c) {
-        if (hipEventSynchronize(ev[c]) != hipSuccess) { rc = ST_ERR_HIP; break; }
-        const int64_t r0 = c * kRows, r1 = std::min(n, r0 + kRows);
-        for (int64_t i = r0; i < r1; ++i) {
-            const double* row = stage_x + i * d;
-            for (int j = 0; j < d; ++j) {
-                acc[j] = i == 0 ? row[j] : acc[j] + row[j];
-                fn |= (int)(row[j] != row[j]);
-                fi |= (int)(fabs(row[j]) == INFINITY);
-            }
+    if (rc == ST_OK) {
+        switch (d) {   // compile-time d: each column's chain in a register, the row loop unrolled
+            case 2: rc = download_stats<2>(stage_x, n, kRows, ev, loc_out, scl_out, fn, fi); break;
+            case 3: rc = download_stats<3>(stage_x, n, kRows, ev, loc_out, scl_out, fn, fi); break;
+            case 4: rc = download_stats<4>(stage_x, n, kRows, ev, loc_out, scl_out, fn, fi); break;
+            case 5: rc = download_stats<5>(stage_x, n, kRows, ev, loc_out, scl_out, fn, fi); break;
+            case 6: rc = download_stats<6>(stage_x, n, kRows, ev, loc_out, scl_out, fn, fi); break;
+            case 7: rc = download_stats<7>(stage_x, n, kRows, ev, loc_out, scl_out, fn, fi); break;
+            default: rc = download_stats<8>(stage_x, n, kRows, ev, loc_out, scl_out, fn, fi); break;
         }
     }
     for (auto e : ev)
@@ -182,17 +251,7 @@ extern "C" int st_standardize_download(const double* dev_x, int64_t n, int32_t d
         *status = fn ? 1 : 2;
         return ST_OK;
     }
-    const double dn = (double)n;
-    for (int j = 0; j < d; ++j) { l[j] = acc[j] / dn; acc[j] = fabs(stage_x[j] - l[j]); }
-    for (int64_t i = 1; i < n; ++i) {
-        const double* row = stage_x + i * d;
-        __builtin_prefetch(row + 64 * d);
-        for (int j = 0; j < d; ++j) acc[j] += fabs(row[j] - l[j]);
-    }
-    for (int j = 0; j < d; ++j) {
-        if (acc[j] / dn == 0.0) *status = 3;
-        loc_out[j] = l[j];
-        scl_out[j] = acc[j] / dn;
-    }
+    for (int j = 0; j < d; ++j)
+        if (scl_out[j] == 0.0) *status = 3;
     return ST_OK;
 }

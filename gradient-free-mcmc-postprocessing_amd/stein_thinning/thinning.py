@@ -279,13 +279,57 @@ def _early_upload(sample: np.ndarray, gradient: np.ndarray, weights: Optional[np
     return DeviceProblem(sample, gradient, weights, 0.0, 0.0)   # l, tr filled in with the preconditioner
 
 
+def _on_device(a) -> bool:
+    """A ROCm tensor (torch reports HIP devices as 'cuda')."""
+    return bool(getattr(a, 'is_cuda', False))
+
+
+def _download_standardized(sample, gradient):
+    """The drop-in thin's input path for ROCm tensors (float64, one device, standardize=True):
+    the inputs stay where they are.  Only x travels, device to host, into a page-locked buffer
+    (st_standardize_download: NumPy's sequential axis-0 sums of mean / mean |x - loc| as the chunks land,
+    bit-identical), because its statistics and the 'med' subsample are host work; g's NaN / inf check is a
+    device reduction and g is scaled on the device with x (st_layout_soa_scaled) -- never copied to the
+    host.  Errors as _validate_and_standardize raises them (NaNs before infs, either array).  Returns
+    _upload_standardized's tuple (stage_g None: the host g is fetched only if something reads
+    integrand.gradient) or None (other dtypes, two devices, or d = 1 under a changed NumPy bufsize: the
+    host route)."""
+    import ctypes
+    import torch
+    from . import _native as nat
+    _validate_shapes(sample, gradient)
+    n, d = sample.shape
+    if sample.dtype != torch.float64 or gradient.dtype != torch.float64 or sample.device != gradient.device \
+            or (d == 1 and np.getbufsize() != 8192):   # the native d = 1 column sum models the default bufsize
+        return None
+    with torch.cuda.device(sample.device):
+        x = sample.detach().contiguous()
+        g = gradient.detach().contiguous()
+        flags = torch.stack([torch.isnan(g).any(), torch.isinf(g).any()])   # queued before the download
+        stage_x = _host_buffer((n, d))
+        loc, scl = np.empty(d), np.empty(d)
+        status = ctypes.c_int32(0)
+        nat.check(nat.lib().st_standardize_download(nat.ptr(x), n, d, stage_x.ctypes.data, loc.ctypes.data,
+                                                    scl.ctypes.data, ctypes.byref(status), nat.stream_handle()),
+                  'st_standardize_download')
+        g_nan, g_inf = (bool(v) for v in flags.tolist())
+    if status.value == 1 or g_nan:
+        raise ValueError('sample or gradient contains NaNs.')
+    if status.value == 2 or g_inf:
+        raise ValueError('sample or gradient contains infs.')
+    if status.value == 3:
+        raise ValueError('Too few unique samples in smp.')
+    return n, d, scl, stage_x, None, x, g
+
+
 def _upload_standardized(sample, gradient, standardize: bool):
     """The drop-in thin's input path when a HIP device is present, d = 2 .. 8 and n >= 65536:
     st_standardize_upload computes loc / scl on the host while the raw arrays are staged into
     page-locked buffers and copied to the device underneath, then the device lays them out with the
     scaling applied (st_layout_soa_scaled: x / scl, g * scl, the host's bits).  Returns
     (n, d, scl, stage_x, stage_g, x_raw, g_raw) or None (the st_standardize_host route applies).
-    Raises the reference's ValueErrors like _validate_and_standardize."""
+    Raises the reference's ValueErrors like _validate_and_standardize.  ROCm tensor inputs take
+    _download_standardized (no host copy of g)."""
     import ctypes
     if not standardize:
         return None
@@ -296,6 +340,10 @@ def _upload_standardized(sample, gradient, standardize: bool):
     except Exception:   # noqa: BLE001 -- an optimisation only
         return None
     from . import _native as nat
+    if _on_device(sample) and _on_device(gradient):
+        up = _download_standardized(sample, gradient)
+        if up is not None:
+            return up
     sample = np.ascontiguousarray(_as_numpy(sample))
     gradient = np.ascontiguousarray(_as_numpy(gradient))
     _validate_shapes(sample, gradient)
@@ -330,8 +378,8 @@ def _device_integrand(up, preconditioner, weights: Optional[np.ndarray]) -> Stei
     n, d, scl, stage_x, stage_g, x_raw, g_raw = up
     prob = DeviceProblem.from_raw_device(x_raw, g_raw, weights, scl, 0.0, 0.0)
 
-    def materialize():
-        return _validate_and_standardize(stage_x, stage_g, True)
+    def materialize():   # device-tensor inputs (stage_g None): g comes to the host only here
+        return _validate_and_standardize(stage_x, stage_g if stage_g is not None else g_raw, True)
     try:
         # the preconditioner's subsample rows, standardised on the host (x / scl: the same IEEE divisions)
         linv = make_precon_rows(n, d, lambda rows: stage_x[rows] / scl, preconditioner, on_device=True)
@@ -470,19 +518,35 @@ def _guard() -> bool:
     return nat.near_tie_guard()
 
 
+def _home(a):
+    """The device index of a ROCm tensor input, else None."""
+    return a.device.index if _on_device(a) else None
+
+
+def _on_home(a):
+    """Run on the device a ROCm tensor input lives on (its arrays are used in place), else as is."""
+    if _home(a) is None:
+        return contextlib.nullcontext()
+    import torch
+    return torch.cuda.device(a.device)
+
+
 def thin(sample, gradient, n_points: int, standardize: bool = True, preconditioner='id') -> np.ndarray:
-    """Stein thinning: indices of ``n_points`` rows of ``sample`` greedily minimising the KSD."""
-    integrand = _make_stein_integrand(sample, gradient, standardize, preconditioner)
-    return _greedy_search(n_points, integrand)
+    """Stein thinning: indices of ``n_points`` rows of ``sample`` greedily minimising the KSD.  ``sample`` /
+    ``gradient`` may be NumPy arrays or ROCm tensors (used in place on their device: _download_standardized)."""
+    with _on_home(sample):
+        integrand = _make_stein_integrand(sample, gradient, standardize, preconditioner)
+        return _greedy_search(n_points, integrand)
 
 
-def _thin_chains(count: int, build: Callable, n_points) -> list:
+def _thin_chains(count: int, build: Callable, n_points, homes=None) -> list:
     """The per-chain loop ``[thin(...) for each chain]`` with the thins side by side: chain i's integrand is
     ``build(i)`` (validation errors in the loop's order: chain 0's input, then n_points, then the other
     chains'), the chains are dealt round-robin to the GPUs this process may use (all visible ones, or
     the one the device policy pins: _native.select_device_index), and each GPU runs its chains with
     device.greedy_concurrent (one batch launch: each latency-bound thin on a share of the CUs), the GPUs
-    at the same time.  The same indices as the loop."""
+    at the same time; a chain given as ROCm tensors runs on their device (homes[i]).  The same indices as
+    the loop."""
     import torch
     from . import _native as nat
     from .device import greedy_concurrent
@@ -490,7 +554,7 @@ def _thin_chains(count: int, build: Callable, n_points) -> list:
     nat.require_device()
     devs = ([torch.cuda.current_device()] if nat.policy_pinned() or count < 2
             else list(range(torch.cuda.device_count())))
-    owner = [devs[i % len(devs)] for i in range(count)]
+    owner = [devs[i % len(devs)] if homes is None or homes[i] is None else homes[i] for i in range(count)]
     integrands = []
     for i in range(count):
         with torch.cuda.device(owner[i]):
@@ -540,7 +604,8 @@ def thin_chains(samples, gradients, n_points: int, standardize: bool = True, pre
     samples, gradients = list(samples), list(gradients)
     count = _same_length(samples, gradients)
     return _thin_chains(count, lambda i: _make_stein_integrand(samples[i], gradients[i], standardize,
-                                                               preconditioner), n_points)
+                                                               preconditioner), n_points,
+                        [_home(x) for x in samples])
 
 
 def thin_gf_chains(samples, log_ps, log_qs, gradients_q, n_points: int, standardize: bool = True,
@@ -551,12 +616,13 @@ def thin_gf_chains(samples, log_ps, log_qs, gradients_q, n_points: int, standard
     count = _same_length(samples, log_ps, log_qs, gradients_q)
     return _thin_chains(count, lambda i: _make_stein_gf_integrand(samples[i], log_ps[i], log_qs[i], gradients_q[i],
                                                                   standardize, range_cap, preconditioner),
-                        n_points)
+                        n_points, [_home(x) for x in samples])
 
 
 def thin_gf(sample, log_p, log_q, gradient_q, n_points: int, standardize: bool = True,
             range_cap: Optional[float] = None, preconditioner='id') -> np.ndarray:
     """Gradient-free Stein thinning with auxiliary density q (report.tex:390-426)."""
-    integrand = _make_stein_gf_integrand(sample, log_p, log_q, gradient_q, standardize, range_cap,
-                                         preconditioner)
-    return _greedy_search(n_points, integrand)
+    with _on_home(sample):
+        integrand = _make_stein_gf_integrand(sample, log_p, log_q, gradient_q, standardize, range_cap,
+                                             preconditioner)
+        return _greedy_search(n_points, integrand)

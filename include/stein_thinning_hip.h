@@ -421,8 +421,9 @@ int st_standardize_upload(const double *sample, const double *gradient, int64_t 
  * comes back into the page-locked stage_x in 64 K-row chunks on `stream`, each chunk's column sums taken
  * as it lands (NumPy's sequential axis-0 order, bit-identical); loc_out / scl_out as st_standardize_host's.
  * g stays on the device (its NaN / inf check is the caller's).  *status: 0 ok, 1 NaN in x, 2 inf in x, 3 a
- * zero scale.  d = 2 .. 8 and n >= 65536 only (ST_ERR_UNSUPPORTED otherwise).  Returns when x is on the
- * host and the statistics are done. */
+ * zero scale.  Any n >= 1, d >= 1 (outside d = 2 .. 8, n >= 65536: one copy, then st_standardize_host's
+ * column passes; d = 1 assumes NumPy's default bufsize).  Returns when x is on the host and the
+ * statistics are done. */
 int st_standardize_download(const double *dev_x, int64_t n, int32_t d, double *stage_x, double *loc_out,
                             double *scl_out, int32_t *status, void *stream);
 

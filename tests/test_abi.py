@@ -110,6 +110,16 @@ def test_host_side_validation_of_the_newer_entry_points(libpath):
     assert lib.st_standardize_upload(*(st[:4] + [odd] + st[5:])) == inv
     assert lib.st_standardize_upload(*(st[:3] + [9] + st[4:])) == _native.ST_ERR_UNSUPPORTED
     assert lib.st_standardize_upload(*(st[:2] + [1000] + st[3:])) == _native.ST_ERR_UNSUPPORTED
+    # the device-tensor counterpart: NULLs and empty inputs
+    assert lib.st_standardize_download(None, 100, 4, p, p, p, ctypes.byref(status), None) == inv
+    assert lib.st_standardize_download(p, 0, 4, p, p, p, ctypes.byref(status), None) == inv
+    assert lib.st_standardize_download(p, 100, 0, p, p, p, ctypes.byref(status), None) == inv
+    # near-tie guard: the flag read-back's checks, the switch and its read-back (host-only state)
+    step = ctypes.c_int64(0)
+    assert lib.st_greedy_near_tie(None, 4096, ctypes.byref(step), None) == inv
+    assert lib.st_greedy_near_tie(p, 64, ctypes.byref(step), None) == inv
+    assert lib.st_tune_get(20) in (0, 1)
+    assert lib.st_tune_get(999) == -2 ** 31   # INT32_MIN: no such key
     # repeated-row compaction, scaled layout, 'med' distances
     assert lib.st_run_workspace_bytes(1) > 0 and lib.st_run_workspace_bytes(1 << 20) >= 8 + 8 * 1024
     assert lib.st_run_starts(p, p, None, 10, 4, 16, None, p, 1 << 10, None) == inv          # no output
