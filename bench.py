@@ -296,6 +296,80 @@ def dedup_timing(prob, m: int, want_idx, stream, repeats: int = 5):
                     'starts selects the same rows (stein_thinning.device.DeviceProblem.dedup_view)'}
 
 
+def rank_local_ms(integrand, m: int, rank: int, world: int, reps: int = 3):
+    """ms per thin of this rank's shard ALONE on its GPU: the single-device persistent kernel over rows
+    shard_bounds(n, rank, world), no rank exchange (HIP events on the launch stream, median) -- T_local
+    of DESIGN.md section 5's cost model T(N) = T_local(n / N) + H(N) + X."""
+    import torch
+    from stein_thinning import distributed as sd
+    lo, hi = sd.shard_bounds(integrand.n, rank, world)
+    prob = integrand.device_problem().subset(np.arange(lo, hi))
+    idx, a, ws = prob.greedy_buffers(m)
+    prob.greedy_launch(m, idx, a, ws)
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for e0, e1 in evs:
+        e0.record(stream)
+        prob.greedy_launch(m, idx, a, ws)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
+
+
+def rank_hop(ms_sharded: float, integrand, m: int, rank: int, world: int, dev):
+    """The measured rank level per step: (the sharded thin - the slowest rank's shard alone) / m -- H(N) + X
+    of DESIGN.md section 5 (the rank winner's push over xGMI, the peers' polls, the candidate rows and the
+    R-way pick), in one number, on the hardware the run is on.  Collective."""
+    local = _max_over_ranks([rank_local_ms(integrand, m, rank, world)], dev)[0]
+    return {'us_per_step': round((ms_sharded - local) / m * 1e3, 3), 'local_ms_per_thin': round(local, 4),
+            'sharded_ms_per_thin': round(ms_sharded, 4),
+            'note': '(sharded thin - the slowest rank\'s shard thinned alone on its GPU) / m: the rank exchange '
+                    '(H + X of DESIGN.md section 5) per step' +
+                    (' -- ranks SHARE one GPU here (rehearsal): no xGMI in it' if SHARE_DEVICE else '')}
+
+
+def config5_sharded(rank: int, world: int, dev, steps: int = 3):
+    """Config 5 (d = 50, gradient-free, n = 5e5, m = 500: the workload that shards)
+    on the same ranks: ms per thin (max over ranks, barrier-bracketed), the per-rank launch median, its
+    fp64 VALU fraction and the measured rank hop.  Collective; nulls at one rank."""
+    nulls = {'ms_per_thin': None, 'kernel_median_us': None, 'frac': None, 'engine': None, 'rank_hop': None,
+             'note': 'measured only when bench.py runs on N > 1 ranks'}
+    if world == 1:
+        return nulls
+    import torch
+    import torch.distributed as dist
+    from stein_thinning import distributed as sd
+    cfg = CONFIGS['c5']
+    n, m = cfg['n'], cfg['m']
+    integrand, _, _ = make_integrand(cfg)
+    runner = sd.sharded_runner(integrand, m)   # collective; one validated run
+    runner.launch()
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    stream = torch.cuda.current_stream()
+    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(steps)]
+    t0 = time.perf_counter()
+    for e0, e1 in evs:
+        e0.record(stream)
+        runner.launch()
+        e1.record(stream)
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    dist.barrier()
+    med = float(np.median([e0.elapsed_time(e1) for e0, e1 in evs])) * 1e-3
+    elapsed, med = _max_over_ranks([elapsed, med], dev)
+    flop = algorithmic_flop_per_pair(50, True)
+    tflops = n * m / world * flop / med / 1e12
+    ms = elapsed / steps * 1e3
+    return {'ms_per_thin': round(ms, 4), 'kernel_median_us': round(med * 1e6, 1),
+            'frac': round(tflops / FP64_VALU_PEAK_TFS, 4), 'achieved_TFs': round(tflops, 2),
+            'engine': runner.mode, 'n': n, 'd': 50, 'm': m, 'steps': steps,
+            'rank_hop': rank_hop(ms, integrand, m, rank, world, dev) if runner.mode == 'device-exchange' else None,
+            'note': f"config 5 ({cfg['desc']}) row-sharded over the same ranks; frac = algorithmic fp64 "
+                    f"({flop} flop per pair) per rank / the rank's launch median / {FP64_VALU_PEAK_TFS} TF"}
+
+
 # Rehearsal mode (ST_BENCH_SHARE_DEVICE=1, never used by the driver): every rank on cuda:0 and a
 # gloo group, so the N > 1 flow (mailbox setup, device exchange, timing reductions) can run on a
 # one-GPU box with several processes sharing the device.
@@ -381,6 +455,8 @@ def main():
     ap.add_argument('--no-kernel-timing', action='store_true')
     ap.add_argument('--no-graph', action='store_true', help='N > 1: eager per-step launches instead of a HIP graph')
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
+    ap.add_argument('--no-config5', action='store_true',
+                    help='thin workload at N > 1: skip the config5_sharded object (config 5 row-sharded)')
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
     ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
@@ -496,6 +572,12 @@ def main():
         result_idx = idx.cpu().numpy().view(np.uint32)
     else:
         result_idx = runner.indices() if hasattr(runner, 'indices') else runner.backend.indices()
+    # N > 1: the measured rank level of this run and config 5 sharded (nulls at N = 1)
+    hop, c5 = None, config5_sharded(rank, 1, dev)
+    if sharded and world > 1 and runner.mode == 'device-exchange':
+        hop = rank_hop(elapsed / args.steps * 1e3, integrand, m, rank, world, dev)
+    if sharded and world > 1 and not args.no_config5 and args.config == 'c4':
+        c5 = config5_sharded(rank, world, dev)
 
     roofline = None
     cpu = None
@@ -714,6 +796,8 @@ def main():
                        'first_indices': result_idx[:8].tolist()},
             'exchange': exchange,
             'degraded': degraded,
+            'rank_hop': hop,
+            'config5_sharded': c5,
             'roofline': roofline,
             'cpu_baseline': cpu,
             'end_to_end': e2e if rank == 0 and not sharded else None,
