@@ -89,6 +89,8 @@ int main(int argc, char** argv) {
     const int64_t ld = (n + 63) / 64 * 64;
     hipStream_t s;
     CK(hipStreamCreate(&s));
+    // near-tie guard (st_tune key 20; on by default in the library): PROBE_GUARD=0 times the plain kernels
+    if (getenv("PROBE_GUARD")) st_tune(20, atoi(getenv("PROBE_GUARD")));
     double *x, *g, *A, *out;
     CK(hipMalloc(&x, sizeof(double) * d * ld));
     CK(hipMalloc(&g, sizeof(double) * d * ld));
