@@ -296,6 +296,17 @@ def dedup_timing(prob, m: int, want_idx, stream, repeats: int = 5):
                     'starts selects the same rows (stein_thinning.device.DeviceProblem.dedup_view)'}
 
 
+def _set_guard(enabled) -> bool:
+    """stein_thinning's near-tie guard switch; False when the library predates it (an A/B build loaded
+    through ST_HIP_LIB), which then runs unguarded whatever is asked."""
+    from stein_thinning import _native as nat
+    try:
+        nat.set_near_tie_guard(enabled)
+        return True
+    except ValueError:
+        return False
+
+
 def rank_local_ms(integrand, m: int, rank: int, world: int, reps: int = 3):
     """ms per thin of this rank's shard ALONE on its GPU: the single-device persistent kernel over rows
     shard_bounds(n, rank, world), no rank exchange (HIP events on the launch stream, median) -- T_local
@@ -531,7 +542,7 @@ def main():
     # the headline leg: st_greedy over all n rows as the kernel computes them (compact arithmetic: no
     # near-tie flag, unless --headline-guard).  The drop-in thin's default (guard on) is timed beside it:
     # "near_tie_guard" (all rows) and "dedup" (the run starts, the drop-in's path on repeated rows).
-    nat.set_near_tie_guard(bool(args.headline_guard))
+    _set_guard(bool(args.headline_guard))
 
     if not sharded:
         prob = integrand.device_problem()
@@ -690,8 +701,9 @@ def main():
                 run_once()   # leave the buffers as the timed (compact) run left them
                 torch.cuda.synchronize()
         guarded = None
-        nat.set_near_tie_guard(None)   # the drop-in default from here on (ST_NEAR_TIE, on unless '0')
-        if world == 1 and not sharded and d in (2, 4) and arithmetic == 'compact' and nat.near_tie_guard():
+        guard_lib = _set_guard(None)   # the drop-in default from here on (ST_NEAR_TIE, on unless '0')
+        if world == 1 and not sharded and d in (2, 4) and arithmetic == 'compact' and nat.near_tie_guard() \
+                and guard_lib:
             # the same thin of all n rows with the near-tie guard (not `value`): its time and first
             # flagged step (-1 none; rows that repeat their predecessor tie exactly, so a raw MCMC sample
             # is flagged at once -- the drop-in thins its run starts instead, "dedup")
@@ -735,15 +747,18 @@ def main():
             xd = torch.from_numpy(np.ascontiguousarray(host_x)).to(dev)
             gd = torch.from_numpy(np.ascontiguousarray(host_g)).to(dev)
             torch.cuda.synchronize()
-            st.thin(xd, gd, m, preconditioner='med')
-            dts = []
-            for _ in range(3):
-                t_e = time.perf_counter()
-                dev_idx = st.thin(xd, gd, m, preconditioner='med')
-                dts.append(time.perf_counter() - t_e)
-            e2e['thin_device_tensors_s'] = round(float(np.median(dts)), 4)
-            e2e['device_tensors_runs_s'] = [round(v, 4) for v in dts]
-            e2e['device_tensors_same_indices'] = bool(np.array_equal(dev_idx, result_idx))
+            try:
+                st.thin(xd, gd, m, preconditioner='med')
+                dts = []
+                for _ in range(3):
+                    t_e = time.perf_counter()
+                    dev_idx = st.thin(xd, gd, m, preconditioner='med')
+                    dts.append(time.perf_counter() - t_e)
+                e2e['thin_device_tensors_s'] = round(float(np.median(dts)), 4)
+                e2e['device_tensors_runs_s'] = [round(v, 4) for v in dts]
+                e2e['device_tensors_same_indices'] = bool(np.array_equal(dev_idx, result_idx))
+            except nat.HipExtensionError:   # an A/B build (ST_HIP_LIB) older than the device-tensor path
+                e2e['thin_device_tensors_s'] = None
             del xd, gd
 
     exchange, degraded = None, False

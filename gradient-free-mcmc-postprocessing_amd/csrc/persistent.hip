@@ -12,6 +12,8 @@ namespace st {
 // replicas each starts on a fresh 512-B boundary plus 256 B, so their lines fall on other channels
 // the GUARD instantiations (persistent_guard.hip): the kernel for a plan, or nullptr
 const void* guarded_persistent_fn(int d, bool gf, int rt, int nt, int bpc, bool gen, bool batch);
+// the small-shard instantiations (persistent_small.hip: 256 threads, 1 / 2 register rows), or nullptr
+const void* small_persistent_fn(int d, bool gf, int rt, bool cmp, bool batch, bool guard);
 
 int64_t persistent_rep_stride(int G, int rec_stride, int nrep) {
     const int64_t one = (int64_t)G * rec_stride;
@@ -164,7 +166,11 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     // plan (tie_bounds set: compact, one device) takes the GUARD instantiation of persistent_guard.hip
     const void* fn;
     const bool guarded = b ? b->p[0].tie_bounds != nullptr : a.tie_bounds != nullptr;
-    if (guarded) {
+    if constexpr (RT < 4 && D <= kMaxCtDim) {   // small shards: compiled in persistent_small.hip
+        static_assert(NT == 256 && BPC == 1 && GEN, "small-shard plans only");
+        fn = small_persistent_fn(D, GF, RT, arith_compact(), b != nullptr, guarded);
+        if (!fn) return hipErrorNotSupported;
+    } else if (guarded) {
         if constexpr (D <= kMaxCtDim) {
             fn = guarded_persistent_fn(D, GF, RT, NT, BPC, GEN, b != nullptr);
             if (!fn) return hipErrorNotSupported;
@@ -234,6 +240,8 @@ static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int
         return launch_p<D, GF, 8, 512>(a, G, lds, s, dry, b);
     }
     switch (rt) {
+        case 1: return launch_p<D, GF, 1, 256>(a, G, lds, s, dry, b);
+        case 2: return launch_p<D, GF, 2, 256>(a, G, lds, s, dry, b);
         case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s, dry, b);
         case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s, dry, b);
         default: return launch_p<D, GF, 16, 256>(a, G, lds, s, dry, b);
@@ -324,10 +332,14 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     if (!wide && g_persist_nt <= 0 && bpc == 1 && R > kNt512MinRows) nt = 512;
     const int rt_max = (nt == 512 || bpc == 2) ? 8 : 16;
     int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
-    if (rt != 4 && rt != 6 && rt != 8 && rt != 16) rt = rt_max;
+    const bool small_ok = nt == 256 && bpc == 1 && !wide;   // 1 / 2 register rows: persistent_small.hip
+    if (rt != 4 && rt != 6 && rt != 8 && rt != 16 && !(small_ok && (rt == 1 || rt == 2))) rt = rt_max;
     if (rt > rt_max) rt = rt_max;
     if (rt == 6 && (nt != 512 || bpc == 2)) rt = 8;
     while (rt > 4 && (int64_t)rt * nt > R) rt = rt == 6 ? 4 : rt / 2;   // no empty register rows
+    // small shards: the fewest register rows that hold the block's rows (padding rows compute like real
+    // ones; 1 / 2 rows per thread at <= 256 / 512 rows per block)
+    if (small_ok && g_persist_rt <= 0 && R <= 2 * 256) rt = R <= 256 ? 1 : 2;
     if (wide) rt = 1;
     const bool gf = w != nullptr;
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);

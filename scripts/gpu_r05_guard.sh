@@ -14,13 +14,12 @@ ab() {   # ab <tag> <config> <steps>
   for r in 1 2; do
     ST_NEAR_TIE=0 ST_HIP_LIB=tools/_diag/ab/r04/libstein_hip.so timeout -k 10 300 python3 bench.py --config $cfg \
       --steps $steps --warmup 2 --no-cpu-baseline --no-kernel-timing > gpurun_out/r05g/${tag}_A$r.json 2> gpurun_out/r05g/${tag}_A$r.err || return 1
-    timeout -k 10 300 python3 bench.py --config $cfg --steps $steps --warmup 2 --no-cpu-baseline --no-kernel-timing \
+    ST_NEAR_TIE=${GUARD_B:-1} timeout -k 10 300 python3 bench.py --config $cfg --steps $steps --warmup 2 --no-cpu-baseline --no-kernel-timing \
       > gpurun_out/r05g/${tag}_B$r.json 2> gpurun_out/r05g/${tag}_B$r.err || return 1
   done
   for f in ${tag}_A1 ${tag}_B1 ${tag}_A2 ${tag}_B2; do
     python3 -c "import json; d=json.loads(open('gpurun_out/r05g/$f.json').read().strip().splitlines()[-1]); r=d['roofline']; print('$f', round(d['ms_per_step'],4), r.get('kernel_median_us'), (d.get('dedup') or {}).get('near_tie_step'), (d.get('dedup') or {}).get('thin_s'), (d.get('end_to_end') or {}).get('thin_host_arrays_s'))"
   done
 }
-ab c4 c4 20 || exit 1
-ab c2 c2 30 || exit 1
+for spec in ${AB:-c4:20 c2:30}; do ab ${spec%%:*} ${spec%%:*} ${spec##*:} || exit 1; done
 echo done
