@@ -62,14 +62,14 @@ struct Scratch {          // small per-block scratch at the start of the dynamic
 };
 
 // near-tie guard state (GUARD kernels only: after Scratch in the dynamic LDS), by step parity: the
-// rescan's per-wave minimum, its row and the wave's second-smallest sum; the step's winner (row, sum,
-// score row and weight) and this block's published minimum; the threshold recurrence
+// rescan's per-wave minimum, its row and the wave's second-smallest sum; the step's winner (row and sum;
+// its score row and weight are read from Scratch::row, which holds them until the next pick) and this
+// block's published minimum; the threshold recurrence
 struct GuardScratch {
     double rs_min[2][kMaxPWaves], rs_run[2][kMaxPWaves];
     uint32_t rs_idx[2][kMaxPWaves];
     uint32_t win_i[2];
     double win_v[2], blk_v[2];
-    double win_row[2][kMaxCtDim + 1];
     double tg[6];         // recurrence state (stein_ref.c tie_state): c1, wmax, Dmax, Q, E, thr
     double bnd[kMaxPWaves][2];   // per wave: max_i |g_i|^2, max_i w_i^2 over its rows (staging)
     // 512-thread kernels: wave 0's per-lane rescan of its register rows (step t - 1, written at the start
@@ -338,8 +338,9 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
             uint64_t k;
             uint32_t ib;
             combine_waves<NT>(sc, k, ib);
-            sc->vblk = key_value(k);   // read by every thread after wait_and_pick's barrier
-            if constexpr (GUARD) gsc->blk_v[t & 1] = sc->vblk;   // this block's minimum of step t
+            const double vb = key_value(k);
+            sc->vblk = vb;   // read by every thread after wait_and_pick's barrier
+            if constexpr (GUARD) gsc->blk_v[t & 1] = vb;   // this block's minimum of step t
             uint64_t* gr = a.gran + (t & 1) * a.rep_stride + (int64_t)bid * a.rec_stride;
             const uint64_t tag = step_tag(t);
             __hip_atomic_store(gr + 0, tag | (k >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -354,8 +355,9 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
         uint32_t ib;
         combine_waves<NT>(sc, k, ib);
         if (threadIdx.x == 0) {
-            sc->vblk = key_value(k);
-            if constexpr (GUARD) gsc->blk_v[t & 1] = sc->vblk;   // this block's minimum of step t
+            const double vb = key_value(k);
+            sc->vblk = vb;
+            if constexpr (GUARD) gsc->blk_v[t & 1] = vb;   // this block's minimum of step t
         }
         if ((int)threadIdx.x < a.nrep) {
             const uint64_t tag = step_tag(t);
@@ -457,8 +459,8 @@ __device__ __forceinline__ void top2_wave(GuardScratch* sc, const Top2& r, int p
 // (stein_ref.c tie_init / tie_step, the same operations).  Step 0 first reads the problem's bounds,
 // which every block merged before publishing step 0 (so this block's sweep of step 0 saw them all)
 template <int D, bool GF>
-__device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc, int64_t t, int64_t r0,
-                                          int64_t r1, int nwaves) {
+__device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc, const double* row, int64_t t,
+                                          int64_t r0, int64_t r1, int nwaves) {
     const int par = (int)(t & 1);
     double* ts = sc->tg;   // c1, wmax, Dmax, Q, E, thr
     if (t == 0) {   // stein_ref.c tie_init
@@ -491,7 +493,7 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
         __hip_atomic_fetch_max(a.tie, ~(unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const double Q = ts[3] + v;
-    const double* gj = sc->win_row[par];
+    const double* gj = row + D;   // the winner's g (and w), in Scratch::row until the next pick
     double gj2 = gj[0] * gj[0];
 #pragma unroll
     for (int k = 1; k < D; ++k) gj2 = gj2 + gj[k] * gj[k];
@@ -511,7 +513,7 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
 // the in-order vmcnt wait in front of the row's use.  After the wave MINLOC the winning lane
 // writes the row to sc->row.  Returns the winner's index, or -1 if the sweep timed out (grid-wide
 // abort).
-// guard: the near-tie bookkeeping of this step -- the winner's row, sum and score row in slot t & 1 --
+// guard: the near-tie bookkeeping of this step -- the winner's row and sum in slot t & 1 --
 // and, with rescan_here, rescan0() (wave 0's register rows, while the first poll is in flight; the
 // 512-thread kernels rescan them at the start of the next step instead, away from the sweep's registers)
 struct NoRescan {
@@ -781,12 +783,6 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
                 if (row_of != gi) load_row(gi);
 #pragma unroll
                 for (int k = 0; k < kRow; ++k) sc->row[k] = rowv[k];
-                if constexpr (GUARD) {   // the near-tie check of this step (one step later) needs its g, w
-                    if (guard) {
-#pragma unroll
-                        for (int k = 0; k < D + (GF ? 1 : 0); ++k) gsc->win_row[t & 1][k] = rowv[D + k];
-                    }
-                }
             }
         }
         if constexpr (kWide) {   // the winner is wave-uniform now: 64 lanes fetch its 2d (+1) values
@@ -1411,7 +1407,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         if constexpr (GUARD) {
             if (guard && tid >= 64) {   // off the critical path: these waves only wait for the sweep now
                 if (tid < 128 && !(a.tie_dbg & 4)) reduce_w0(t - 1);   // wave 0's lanes of step t - 1
-                if (tid == 64 && !(a.tie_dbg & 2)) tie_check<D, GF>(a, gsc, t - 1, r0, r1, kNW);
+                if (tid == 64 && !(a.tie_dbg & 2)) tie_check<D, GF>(a, gsc, sc->row, t - 1, r0, r1, kNW);
                 if (!(a.tie_dbg & 1)) rescan_rest(t);
             }
         }
@@ -1432,7 +1428,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         }
         if (guard && tid >= 64 && tid < 128 && done == a.m + 1) reduce_w0(a.m - 1);
         if (guard && tid == 64 && done == a.m + 1) {
-            tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW);
+            tie_check<D, GF>(a, gsc, sc->row, a.m - 1, r0, r1, kNW);
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)
                 double* st_out = const_cast<double*>(a.tie_bounds) + 2;
                 st_out[0] = gsc->tg[3];
