@@ -68,7 +68,6 @@ static int g_persist_delay = -1;
 // measured and dropped: the extra live registers spilled inside the step loop (75 VGPRs of scratch)
 // and every variant ran at 8.6-8.7 ms (profiles/r04_lds_interleaved_rejected.log)
 static int g_persist_lds2 = -1;
-static int g_tie_dbg = 0;        // st_tune key 21 (PersistArgs::tie_dbg; measurement only)
 // automatic register rows of the compact-only kernel: 9 (28 B of scratch at d = 4) unless more than
 // kCmpStreamRows rows per block would still be streamed, then 10 (108 B of scratch; the streamed
 // rows then no longer stay in the XCD's L2).  Same-box, d = 4, m = 1000 (profiles/r03_compact_only_rt.log):
@@ -92,7 +91,6 @@ int persistent_tune_get(int key) {
         case 15: return g_persist_sal;
         case 16: return g_persist_delay;
         case 19: return g_persist_lds2;
-        case 21: return g_tie_dbg;
         default: return INT32_MIN;
     }
 }
@@ -146,11 +144,6 @@ int persistent_tune(int key, int value) {
     if (key == 19) {
         if (value < -1 || value > 1) return -1;
         g_persist_lds2 = value;
-        return 0;
-    }
-    if (key == 21) {
-        if (value < 0 || value > 63) return -1;
-        g_tie_dbg = value;
         return 0;
     }
     return -1;
@@ -387,7 +380,6 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     if (guard) {
         a.tie_bounds = reinterpret_cast<const double*>(p + kWsBoundsOff);
         a.tie = reinterpret_cast<unsigned*>(p + kWsTieOff);
-        a.tie_dbg = g_tie_dbg;
     }
     a.gran = reinterpret_cast<uint64_t*>(p + kWsControlBytes);
     a.rows_per_block = R;

@@ -231,9 +231,6 @@ struct PersistArgs {
     // an atomic max (0: none); tie[3] = 1 marks a guarded run
     const double* tie_bounds;
     unsigned* tie;
-    int tie_dbg;          // st_tune key 21 (measurement only): 1 skip the waves' rescans, 2 skip the check,
-                          // 4 skip wave 0's rescan, 8 / 16 the streamed / LDS rows', 32 the bounds pass
-                          // (the guard's verdict is then meaningless)
 };
 
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
@@ -897,10 +894,13 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     const int64_t str_base = lds_base + RL;
     const double l = a.l, l2 = a.l * a.l, m3l2 = -3.0 * l2, tr = a.tr;
     const int lok = CMP ? scale_in_range(l, tr) : 0;   // compact: the per-problem part of the rule
-    // near-tie guard (GUARD kernels; module comment above tie_check)
-    const bool guard = GUARD && CMP && !kWide && a.tie_bounds != nullptr;
-    if constexpr (GUARD) {
-        if (guard && tid == 0) {
+    // near-tie guard (GUARD kernels, launched only with a.tie_bounds set; module comment above tie_check).
+    // Compile-time, and its wave conditions on the wave index in an SGPR (scalar branches): runtime
+    // flags and per-lane masks here cost SGPRs that spill into VGPR lanes on the exchange's path
+    constexpr bool guard = GUARD && CMP && !kWide;
+    const int wid = __builtin_amdgcn_readfirstlane((int)tid >> 6);
+    if constexpr (guard) {
+        if (tid == 0) {
             gsc->tied = 0;
             if (bid() == 0) a.tie[3] = 1u;   // a guarded run (st_greedy_near_tie)
         }
@@ -951,7 +951,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         // g_i0 g_i0 + g_i1 g_i1 + ... and of w_i w_i over this block's rows, a NaN as +inf, merged into the
         // problem's words with u64 atomic maxima that complete before any record of this block is
         // published (the fence) -- so a block that has seen every step-0 record sees the final bounds
-        if (guard && !(a.tie_dbg & 32)) {
+        {
             double gm = 0.0, wm = GF ? 0.0 : 1.0;
             auto take_row = [&](double s2, double wv) {
                 gm = __builtin_fmax(gm, __builtin_isnan(s2) ? INFINITY : s2);
@@ -993,7 +993,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     if constexpr (GUARD && !kWide) {
         // one atomic pair per block; their latency overlaps step 0's diagonal, and the release fence
         // in front of publish(0) orders them before this block's step-0 record (written by wave 0)
-        if (guard && tid == 0 && !(a.tie_dbg & 32)) {
+        if (tid == 0) {
             double gm = gsc->bnd[0][0], wm = gsc->bnd[0][1];
             for (int w = 1; w < NT / 64; ++w) {
                 gm = __builtin_fmax(gm, gsc->bnd[w][0]);
@@ -1054,7 +1054,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         }
     }
     if constexpr (GUARD) {
-        if (guard && tid < 64) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the bounds (above)
+        if (wid == 0) __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");   // the bounds (above)
     }
     publish<NT, GUARD>(a, sc, bv, bi, 0, r1, bid(), gsc);
 
@@ -1074,12 +1074,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         Top2 r;
         rescan_regs(r);
         if constexpr (!kWide) {
-            if (!(a.tie_dbg & 16))
-                for (int e = tid - 64; e < RL; e += kPBlock - 64)
-                    if (lds_base + e < r1) r.add(lrow(e)[fA], (uint32_t)(lds_base + e));
-            if (!(a.tie_dbg & 8))
-                for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64)
-                    r.add((kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row], (uint32_t)row);
+            for (int e = tid - 64; e < RL; e += kPBlock - 64)
+                if (lds_base + e < r1) r.add(lrow(e)[fA], (uint32_t)(lds_base + e));
+            for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64)
+                r.add((kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row], (uint32_t)row);
         }
         top2_wave(gsc, r, (int)(tt & 1));
     };
@@ -1098,18 +1096,18 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         r.bi = gsc->w0_bi[tid - 64];
         top2_wave(gsc, r, (int)(tt & 1), 0);
     };
-    if constexpr (GUARD) {
-        if (guard && tid >= 64 && !(a.tie_dbg & 1)) rescan_rest(0);
+    if constexpr (guard) {
+        if (wid >= 1) rescan_rest(0);
     }
 
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
     int64_t t = 1;
     for (; t < a.m; ++t) {
         const int64_t win = wait_and_pick<D, GF, kMaxG, GUARD>(a, sc, t - 1, bid(), G(), gsc, guard,
-                                                               guard && !kDyn && !(a.tie_dbg & 4), rescan_w0);
+                                                               guard && !kDyn, rescan_w0);
         if (win < 0) break;
-        if constexpr (GUARD && kDyn) {   // wave 0's register rows of step t - 1: per lane into LDS (wave 1
-            if (guard && tid < 64 && !(a.tie_dbg & 4)) rescan_w0();   // reduces them after publish(t))
+        if constexpr (guard && kDyn) {   // wave 0's register rows of step t - 1: per lane into LDS (wave 1
+            if (wid == 0) rescan_w0();   // reduces them after publish(t))
         }
         if (bid() == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
         // chunk counter of the NEXT step (its last use, step t - 1, ended before publish's barrier)
@@ -1404,11 +1402,13 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         ST_STAMP(a, t, 3);
         publish<NT, GUARD>(a, sc, bv, bi, t, r1, bid(), gsc);
         ST_STAMP(a, t, 4);
-        if constexpr (GUARD) {
-            if (guard && tid >= 64) {   // off the critical path: these waves only wait for the sweep now
-                if (tid < 128 && !(a.tie_dbg & 4)) reduce_w0(t - 1);   // wave 0's lanes of step t - 1
-                if (tid == 64 && !(a.tie_dbg & 2)) tie_check<D, GF>(a, gsc, sc->row, t - 1, r0, r1, kNW);
-                if (!(a.tie_dbg & 1)) rescan_rest(t);
+        if constexpr (guard) {
+            if (wid >= 1) {   // off the critical path: these waves only wait for the sweep now
+                if (wid == 1) {
+                    reduce_w0(t - 1);   // wave 0's lanes of step t - 1
+                    if (tid == 64) tie_check<D, GF>(a, gsc, sc->row, t - 1, r0, r1, kNW);
+                }
+                rescan_rest(t);
             }
         }
     }
@@ -1421,13 +1421,13 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             done = a.m + 1;
         }
     }
-    if constexpr (GUARD) {
-        if (kDyn && guard && done == a.m + 1) {
-            if (tid < 64) rescan_w0();
+    if constexpr (guard) {
+        if (kDyn && done == a.m + 1) {
+            if (wid == 0) rescan_w0();
             __syncthreads();
         }
-        if (guard && tid >= 64 && tid < 128 && done == a.m + 1) reduce_w0(a.m - 1);
-        if (guard && tid == 64 && done == a.m + 1) {
+        if (wid == 1 && done == a.m + 1) reduce_w0(a.m - 1);
+        if (tid == 64 && done == a.m + 1) {
             tie_check<D, GF>(a, gsc, sc->row, a.m - 1, r0, r1, kNW);
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)
                 double* st_out = const_cast<double*>(a.tie_bounds) + 2;
