@@ -274,7 +274,7 @@ struct Plan {
 static hipError_t plan_persistent(const double* x, const double* g, const double* w, double* A, int64_t n,
                                   int d, int64_t ld, double l, double tr, int64_t m, uint32_t* idx_out,
                                   void* ws, int64_t ws_bytes, hipStream_t s, int* used, const RankSpec* rs,
-                                  bool plan_only, int grid_cap, Plan& P) {
+                                  bool plan_only, int grid_cap, Plan& P, int rt_force = 0) {
     const RankSpec one{0, n, 0, 1, 0, nullptr, {}};
     if (!rs) rs = &one;
     // 32-bit row indices, padding rows included (< n + one block's register rows)
@@ -324,7 +324,7 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     // scripts/sweep_nt_crossover.sh)
     if (!wide && g_persist_nt <= 0 && bpc == 1 && R > kNt512MinRows) nt = 512;
     const int rt_max = (nt == 512 || bpc == 2) ? 8 : 16;
-    int rt = g_persist_rt > 0 ? g_persist_rt : rt_max;
+    int rt = rt_force > 0 ? rt_force : (g_persist_rt > 0 ? g_persist_rt : rt_max);
     const bool small_ok = nt == 256 && bpc == 1 && !wide;   // 1 / 2 register rows: persistent_small.hip
     if (rt != 4 && rt != 6 && rt != 8 && rt != 16 && !(small_ok && (rt == 1 || rt == 2))) rt = rt_max;
     if (rt > rt_max) rt = rt_max;
@@ -332,7 +332,7 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     while (rt > 4 && (int64_t)rt * nt > R) rt = rt == 6 ? 4 : rt / 2;   // no empty register rows
     // small shards: the fewest register rows that hold the block's rows (padding rows compute like real
     // ones; 1 / 2 rows per thread at <= 256 / 512 rows per block)
-    if (small_ok && g_persist_rt <= 0 && R <= 2 * 256) rt = R <= 256 ? 1 : 2;
+    if (small_ok && g_persist_rt <= 0 && rt_force <= 0 && R <= 2 * 256) rt = R <= 256 ? 1 : 2;
     if (wide) rt = 1;
     const bool gf = w != nullptr;
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);
@@ -491,15 +491,32 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
     BatchArgs bc{}, bg{};
     bc.count = bg.count = count;
     size_t lds = 0, lds_c = 0;
+    // plans that differ only in the small-shard register rows (256 threads, 1 / 2 / 4 rows per thread)
+    // are planned again with the largest of them: one kernel for the batch
+    int rt_force = 0;
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        bool rt_only = true;
+        int rt_max_seen = 0;
+        for (int q = 0; q < count; ++q) {
+            int u = 0;
+            hipError_t e = plan_persistent(pr[q].x, pr[q].g, pr[q].w, pr[q].A, pr[q].n, d, pr[q].ld, pr[q].l,
+                                           pr[q].tr, m, pr[q].idx_out, pr[q].ws, pr[q].ws_bytes, s, &u, nullptr, false,
+                                           cap, P[q], rt_force);
+            if (e != hipSuccess) return e;
+            const Plan& p0 = P[0];
+            if (P[q].wide || P[q].nt != p0.nt || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].use_cmp != p0.use_cmp ||
+                (p0.use_cmp && P[q].rt_c != p0.rt_c))
+                return hipErrorNotSupported;
+            rt_max_seen = std::max(rt_max_seen, P[q].rt);
+            if (P[q].rt != p0.rt && !(P[q].nt == 256 && P[q].rt <= 4 && p0.rt <= 4)) rt_only = false;
+        }
+        bool same = true;
+        for (int q = 1; q < count; ++q) same &= P[q].rt == P[0].rt;
+        if (same) break;
+        if (!rt_only || attempt == 1) return hipErrorNotSupported;
+        rt_force = rt_max_seen;
+    }
     for (int q = 0; q < count; ++q) {
-        int u = 0;
-        hipError_t e = plan_persistent(pr[q].x, pr[q].g, pr[q].w, pr[q].A, pr[q].n, d, pr[q].ld, pr[q].l, pr[q].tr,
-                                       m, pr[q].idx_out, pr[q].ws, pr[q].ws_bytes, s, &u, nullptr, false, cap, P[q]);
-        if (e != hipSuccess) return e;
-        const Plan& p0 = P[0];
-        if (P[q].wide || P[q].nt != p0.nt || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].rt != p0.rt ||
-            P[q].use_cmp != p0.use_cmp || (p0.use_cmp && P[q].rt_c != p0.rt_c))
-            return hipErrorNotSupported;
         P[q].a.stamps = P[q].ac.stamps = nullptr;
         bc.blk_begin[q + 1] = bg.blk_begin[q + 1] = bc.blk_begin[q] + P[q].G;
         lds = std::max(lds, P[q].lds);

@@ -14,8 +14,8 @@ declare -A ARGS=( [energy]="--workload energy" [ksd_c2]="--workload ksd" [proxy_
                   [chains_batch]="--workload chains" )
 declare -A KERN=( [energy]="dist_colsum_kernel" [ksd_c2]="ksd_colsum_kernel" [proxy_gauss]="proxy_mfma_buf_kernel"
                   [proxy_t]="proxy_mfma_buf_kernel" [lv]="lv_kernel<10>"
-                  [c4_persistent]="greedy_persistent<4, false, 9, 512, 1, true, false, st::PersistArgs>" [lv2]="lv_dense_kernel"
-                  [chains_batch]="st::BatchArgs>" )
+                  [c4_persistent]="greedy_persistent<4, false, 9, 512, 1, true, false, st::PersistArgs, false>" [lv2]="lv_dense_kernel"
+                  [chains_batch]="st::BatchArgs, " )
 declare -A EXCL=( [c4_persistent]="@none@" [lv2]="@none@" [chains_batch]="@none@" )
 KEYS=("$@")
 [[ ${#KEYS[@]} -gt 0 ]] || KEYS=(energy ksd_c2 proxy_gauss proxy_t lv)
