@@ -528,7 +528,8 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
     ST_STAMP(a, t + 1, 0);
     if (threadIdx.x < 64) {
         const int lane = threadIdx.x;
-        const uint64_t* bank = a.gran + ((t & 1) * a.nrep + (int)bid % a.nrep) * a.rep_stride;
+        // nrep is a power of two (the plan's): a mask, not an integer division on the exchange's path
+        const uint64_t* bank = a.gran + ((t & 1) * a.nrep + ((int)bid & (a.nrep - 1))) * a.rep_stride;
         const uint64_t want = step_tag(t);
         const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
         const uint64_t wait_limit = (t == 0 && a.nranks == 1) ? kFirstStepTimeoutTicks : kTimeoutTicks;

@@ -12,7 +12,7 @@ fi
 ab() {   # ab <tag> <config> <steps>
   local tag=$1 cfg=$2 steps=$3
   for r in 1 2; do
-    ST_NEAR_TIE=0 ST_HIP_LIB=tools/_diag/ab/r04/libstein_hip.so timeout -k 10 300 python3 bench.py --config $cfg \
+    ST_NEAR_TIE=${GUARD_A:-0} ST_HIP_LIB=${AB_LIB:-tools/_diag/ab/r04/libstein_hip.so} timeout -k 10 300 python3 bench.py --config $cfg \
       --steps $steps --warmup 2 --no-cpu-baseline --no-kernel-timing > gpurun_out/r05g/${tag}_A$r.json 2> gpurun_out/r05g/${tag}_A$r.err || return 1
     ST_NEAR_TIE=${GUARD_B:-1} timeout -k 10 300 python3 bench.py --config $cfg --steps $steps --warmup 2 --no-cpu-baseline --no-kernel-timing \
       > gpurun_out/r05g/${tag}_B$r.json 2> gpurun_out/r05g/${tag}_B$r.err || return 1
