@@ -1,5 +1,5 @@
 # Round 5: the near-tie guard -- its GPU tests, the full GPU suite, then a same-box A/B of the headline and
-# config-2 thins against the round-4 library (tools/_diag/ab/r04, built from HEAD~ sources; guard off there).
+# config-2 thins against the round-4 library (tools/ab/r04, built from HEAD~ sources; guard off there).
 set -o pipefail
 mkdir -p gpurun_out/r05g
 export TMPDIR=/tmp
@@ -12,7 +12,7 @@ fi
 ab() {   # ab <tag> <config> <steps>
   local tag=$1 cfg=$2 steps=$3
   for r in 1 2; do
-    ST_NEAR_TIE=${GUARD_A:-0} ST_HIP_LIB=${AB_LIB:-tools/_diag/ab/r04/libstein_hip.so} timeout -k 10 300 python3 bench.py --config $cfg \
+    ST_NEAR_TIE=${GUARD_A:-0} ST_HIP_LIB=${AB_LIB:-tools/ab/r04/libstein_hip.so} timeout -k 10 300 python3 bench.py --config $cfg \
       --steps $steps --warmup 2 --no-cpu-baseline --no-kernel-timing > gpurun_out/r05g/${tag}_A$r.json 2> gpurun_out/r05g/${tag}_A$r.err || return 1
     ST_NEAR_TIE=${GUARD_B:-1} timeout -k 10 300 python3 bench.py --config $cfg --steps $steps --warmup 2 --no-cpu-baseline --no-kernel-timing \
       > gpurun_out/r05g/${tag}_B$r.json 2> gpurun_out/r05g/${tag}_B$r.err || return 1

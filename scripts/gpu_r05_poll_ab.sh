@@ -5,7 +5,7 @@ mkdir -p gpurun_out/r05ps
 for cfg in c4 c2 c4r8; do
   for r in 1 2; do
     for v in default ps38 ps52; do
-      lib=""; [[ $v == default ]] || lib=tools/_diag/ab/$v/libstein_hip.so
+      lib=""; [[ $v == default ]] || lib=tools/ab/$v/libstein_hip.so
       ST_HIP_LIB=$lib timeout -k 10 300 python3 bench.py --config $cfg --steps 10 --warmup 2 --no-cpu-baseline \
         --no-kernel-timing > gpurun_out/r05ps/${cfg}_${v}_$r.json 2> gpurun_out/r05ps/${cfg}_${v}_$r.err || exit 1
       python3 -c "import json; d=json.loads(open('gpurun_out/r05ps/${cfg}_${v}_$r.json').read().strip().splitlines()[-1]); print('$cfg $v $r', round(d['ms_per_step'],4), (d.get('dedup') or {}).get('thin_s'))"

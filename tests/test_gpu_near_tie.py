@@ -142,3 +142,20 @@ def test_config2_run_starts_unflagged():
     full, _ = oc.greedy_mt(integrand.sample, integrand.gradient, None, integrand.linv_scale, integrand.linv_trace,
                            cfg['m'])
     np.testing.assert_array_equal(got, full)
+
+
+@pytest.mark.parametrize('n', [100_000, 300_000, 600_000])
+def test_dropin_equals_numpy_on_near_ties_at_scale(n):
+    """The near-tie twins planted in samples of 1e5 .. 6e5 rows: every persistent plan the drop-in takes
+    at those sizes (the two-row small-shard kernel, 256-thread blocks with LDS rows, 512-thread blocks
+    with dynamic chunks) flags the construction and the default thin returns NumPy's indices."""
+    X, G, steps = mr.near_tie_twins(3, n=n)
+    want = o.thin(X, G, 20)
+    integrand = st._make_stein_integrand(X, G)
+    np.testing.assert_array_equal(st._greedy_search(20, integrand), want)
+    tie = integrand.device_problem().near_tie
+    assert tie is not None and 0 <= tie <= steps[0]
+    idx, step, _ = _compact_run(integrand.device_problem(), 20)
+    _, _, _, _, flagged = oc.greedy_ties(integrand.sample, integrand.gradient, None, integrand.linv_scale,
+                                         integrand.linv_trace, 20)
+    assert step == np.flatnonzero(flagged)[0]
