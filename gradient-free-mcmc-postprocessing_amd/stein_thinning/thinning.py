@@ -401,6 +401,11 @@ def _attach(integrand: SteinIntegrand, prob) -> SteinIntegrand:
 
 
 def _make_stein_integrand(sample, gradient, standardize: bool = True, preconditioner='id') -> SteinIntegrand:
+    with _on_home(sample):   # ROCm tensors: the problem lives on their device
+        return _make_stein_integrand_here(sample, gradient, standardize, preconditioner)
+
+
+def _make_stein_integrand_here(sample, gradient, standardize, preconditioner) -> SteinIntegrand:
     up = _upload_standardized(sample, gradient, standardize)
     if up is not None:
         return _device_integrand(up, preconditioner, None)
@@ -412,6 +417,13 @@ def _make_stein_integrand(sample, gradient, standardize: bool = True, preconditi
 
 def _make_stein_gf_integrand(sample, log_p, log_q, gradient_q, standardize: bool = True,
                              range_cap: Optional[float] = None, preconditioner='id') -> SteinIntegrand:
+    with _on_home(sample):   # ROCm tensors: the problem lives on their device
+        return _make_stein_gf_integrand_here(sample, log_p, log_q, gradient_q, standardize, range_cap,
+                                             preconditioner)
+
+
+def _make_stein_gf_integrand_here(sample, log_p, log_q, gradient_q, standardize, range_cap,
+                                  preconditioner) -> SteinIntegrand:
     up = _upload_standardized(sample, gradient_q, standardize)
     if up is None:
         sample, gradient_q = _validate_and_standardize(sample, gradient_q, standardize)
