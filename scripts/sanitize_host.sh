@@ -26,8 +26,9 @@ if [[ $WHAT == all || $WHAT == abi ]]; then
   # host side only: each -fsanitize= directly after -Xarch_host (device code is not instrumented)
   $HIPCC --offload-arch=gfx950 -O1 -g -std=c++17 -ffp-contract=off -Xarch_host -fsanitize=address \
     -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer \
-    -o $OUT/abi_asan tools/sanitize/abi_invalid_check.cpp $CS/capi.hip $CS/greedy.hip $CS/persistent.hip \
-    $CS/pairwise.hip $CS/proxy.hip $CS/kde.hip $CS/lv.hip $CS/host_prep.cpp
+    -o $OUT/abi_asan tools/sanitize/abi_invalid_check.cpp $CS/capi.hip $CS/dedup.hip $CS/precon.hip $CS/greedy.hip \
+    $CS/persistent.hip $CS/persistent_guard.hip $CS/persistent_small.hip $CS/pairwise.hip $CS/proxy.hip $CS/kde.hip \
+    $CS/lv.hip $CS/host_prep.cpp $CS/prep_upload.cpp
   $OUT/abi_asan
 fi
 echo sanitize: done

@@ -14,6 +14,10 @@
 
 #include "../../include/stein_thinning_hip.h"
 
+namespace st {   // host_prep.cpp: x's flags and loc / scl alone (st_standardize_download's general path)
+void column_stats_any(const double* x, int64_t n, int d, double* loc, double* scl, int& nan, int& inf);
+}
+
 static int fails = 0;
 #define CHECK(c, ...) do { if (!(c)) { printf("FAIL %s:%d: ", __FILE__, __LINE__); printf(__VA_ARGS__); printf("\n"); ++fails; } } while (0)
 
@@ -56,6 +60,16 @@ static void run_case(int64_t n, int d, int kind, bool alias, std::mt19937_64& rn
     CHECK(rc == ST_OK, "rc %d (n %lld d %d)", rc, (long long)n, d);
     const int want = kind == 0 ? (zero ? 3 : 0) : kind;
     CHECK(status == want, "status %d want %d (n %lld d %d kind %d)", status, want, (long long)n, d, kind);
+    {   // the x-only statistics give the same flags (x's) and the same loc / scl bits
+        std::vector<double> l2(d), s2(d);
+        int fn = 0, fi = 0;
+        st::column_stats_any(x.data(), n, d, l2.data(), s2.data(), fn, fi);
+        CHECK(fn == (kind == 1) && fi == 0, "column_stats_any flags %d %d (kind %d)", fn, fi, kind);
+        if (kind == 0 && status == 0)
+            for (int j = 0; j < d; ++j)
+                CHECK(l2[j] == loc[j] && s2[j] == scl[j], "column_stats_any loc/scl[%d] (n %lld d %d)", j,
+                      (long long)n, d);
+    }
     if (kind != 0 || status != 0) return;
     const std::vector<double>& gx = alias ? xs : xout;
     const std::vector<double>& gg = alias ? gs : gout;
