@@ -339,7 +339,9 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     // near-tie guard: one device, the compact arithmetic, d = 2 / 4 (st_tune key 20) -- the GUARD kernels,
     // whose LDS holds the guard's scratch after Scratch
     const bool guard = tie_guard() && arith_compact() && !wide && rs->nranks == 1 && !plan_only;
-    const size_t head = (sizeof(Scratch) + 15) / 16 * 16 + (guard ? (sizeof(GuardScratch) + 15) / 16 * 16 : 0);
+    // (the 256-thread guarded kernels also hold every thread's step record, GuardLanes)
+    const size_t head = (sizeof(Scratch) + 15) / 16 * 16 + (guard ? (sizeof(GuardScratch) + 15) / 16 * 16 : 0) +
+                        (guard && nt != 512 ? (sizeof(GuardLanes) + 15) / 16 * 16 : 0);
     const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) / bpc - 1024;   // static + slack
     // LDS rows (whole 64-row chunks) for rows past the register rows; the 512-thread (dynamic-chunk)
     // kernels also keep every streamed row's running sum in LDS (8 B per row, whole chunks)

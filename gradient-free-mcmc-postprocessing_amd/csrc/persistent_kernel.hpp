@@ -79,6 +79,15 @@ struct GuardScratch {
     int tied;             // a step was flagged (this block's word was written)
 };
 
+// 256-thread GUARD kernels (no dynamic chunks): every thread's (minimum, its row, second-smallest) of a
+// step, by parity, after GuardScratch in the dynamic LDS.  Only the winner's block needs its block's
+// second-smallest sum (tie_check), so only that block reduces these -- the other blocks run no wave
+// reduction for the guard at all
+struct GuardLanes {
+    double b[2][256], b2[2][256];
+    uint32_t bi[2][256];
+};
+
 // Per-thread argmin scan: every thread visits its rows in increasing index order, so a candidate
 // replaces the running best only if strictly smaller, or NaN over non-NaN (np.argmin order
 // restricted to increasing indices: ties and later NaNs keep the earlier row).  The running best
@@ -410,6 +419,13 @@ struct Top2 {   // a thread's rows: minimum (lowest row on ties) and second-smal
         b = take ? a : b;
         bi = take ? ia : bi;
     }
+    // another set's (minimum, row, second-smallest): the union's
+    __device__ __forceinline__ void merge(double a, double a2, uint32_t ia) {
+        const bool take = (a < b) | ((a == b) & (ia < bi));
+        b2 = __builtin_fmin(__builtin_fmin(b2, a2), take ? b : a);
+        b = take ? a : b;
+        bi = take ? ia : bi;
+    }
 };
 
 __device__ __forceinline__ double wave_max_f64(double m) {
@@ -500,6 +516,24 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
     ts[3] = Q;
     ts[4] = E;
     ts[5] = 0x1p-50 * (8.0 * ts[2] + E);
+}
+
+// tie_check for the 256-thread GUARD kernels (one whole wave): in the winner's block the wave reduces
+// the block's per-thread (minimum, row, second-smallest) of step t (GuardLanes) into rs slot 0, the
+// other blocks only compare their published minimum; then lane 0 runs tie_check on that one slot
+template <int D, bool GF, int NT>
+__device__ __forceinline__ void tie_check_lanes(const PersistArgs& a, GuardScratch* sc, const GuardLanes* gl,
+                                                const double* row, int64_t t, int64_t r0, int64_t r1) {
+    static_assert(NT <= 256, "GuardLanes holds 256 threads");
+    const int par = (int)(t & 1);
+    const uint32_t gi = sc->win_i[par];
+    if ((int64_t)gi >= r0 && (int64_t)gi < r1) {   // block-uniform
+        Top2 r;
+#pragma unroll
+        for (int k = (int)(threadIdx.x & 63); k < NT; k += 64) r.merge(gl->b[par][k], gl->b2[par][k], gl->bi[par][k]);
+        top2_wave(sc, r, par, 0);
+    }
+    if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, row, t, r0, r1, 1);
 }
 
 // wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
@@ -879,8 +913,12 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     // (ds_read2st64_b64 pairs them) instead of a runtime-stride address per coordinate
     constexpr int kLF = 2 * D + 1 + (GF ? 1 : 0);
     GuardScratch* const gsc = reinterpret_cast<GuardScratch*>(lds + (sizeof(Scratch) + 15) / 16 * 2);
-    double* const srow0 =
-        lds + (sizeof(Scratch) + 15) / 16 * 2 + (GUARD ? (sizeof(GuardScratch) + 15) / 16 * 2 : 0);
+    // the per-thread slots of the 256-thread guarded kernels (GuardLanes), after GuardScratch
+    constexpr bool kLanes = GUARD && !kDyn && !kWide;
+    GuardLanes* const gl = reinterpret_cast<GuardLanes*>(lds + (sizeof(Scratch) + 15) / 16 * 2 +
+                                                         (sizeof(GuardScratch) + 15) / 16 * 2);
+    double* const srow0 = lds + (sizeof(Scratch) + 15) / 16 * 2 + (GUARD ? (sizeof(GuardScratch) + 15) / 16 * 2 : 0) +
+                          (kLanes ? (sizeof(GuardLanes) + 15) / 16 * 2 : 0);
     auto lrow = [&](int e) -> double* { return srow0 + (e >> 6) * (kLF * 64) + (e & 63); };
     constexpr int fX = 0, fG = D * 64, fA = 2 * D * 64, fW = (2 * D + 1) * 64;   // field offsets
     // 512-thread kernels with st_tune key 15 = 1: the streamed rows' running sums live in LDS too,
@@ -1080,15 +1118,30 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64)
                 r.add((kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row], (uint32_t)row);
         }
-        top2_wave(gsc, r, (int)(tt & 1));
+        if constexpr (kLanes) {   // per thread, reduced only in the winner's block (tie_check_lanes)
+            const int par = (int)(tt & 1);
+            gl->b[par][tid] = r.b;
+            gl->b2[par][tid] = r.b2;
+            gl->bi[par][tid] = r.bi;
+        } else {
+            top2_wave(gsc, r, (int)(tt & 1));
+        }
     };
     // wave 0's own rescan leaves one Top2 per lane in LDS; wave 1 reduces them after the next publish
+    int64_t t = 1;   // the step loop's counter (rescan_w0 of the 256-thread kernels files by its parity)
     auto rescan_w0 = [&]() {
         Top2 r;
         rescan_regs(r);
-        gsc->w0_b[tid] = r.b;
-        gsc->w0_b2[tid] = r.b2;
-        gsc->w0_bi[tid] = r.bi;
+        if constexpr (kLanes) {   // inside wait_and_pick(t - 1): the sums of step t - 1
+            const int par = (int)((t - 1) & 1);
+            gl->b[par][tid] = r.b;
+            gl->b2[par][tid] = r.b2;
+            gl->bi[par][tid] = r.bi;
+        } else {
+            gsc->w0_b[tid] = r.b;
+            gsc->w0_b2[tid] = r.b2;
+            gsc->w0_bi[tid] = r.bi;
+        }
     };
     auto reduce_w0 = [&](int64_t tt) {   // wave 1
         Top2 r;
@@ -1102,7 +1155,6 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     }
 
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
-    int64_t t = 1;
     for (; t < a.m; ++t) {
         const int64_t win = wait_and_pick<D, GF, kMaxG, GUARD>(a, sc, t - 1, bid(), G(), gsc, guard,
                                                                guard && !kDyn, rescan_w0);
@@ -1406,8 +1458,12 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         if constexpr (guard) {
             if (wid >= 1) {   // off the critical path: these waves only wait for the sweep now
                 if (wid == 1) {
-                    reduce_w0(t - 1);   // wave 0's lanes of step t - 1
-                    if (tid == 64) tie_check<D, GF>(a, gsc, sc->row, t - 1, r0, r1, kNW);
+                    if constexpr (kLanes) {
+                        tie_check_lanes<D, GF, NT>(a, gsc, gl, sc->row, t - 1, r0, r1);
+                    } else {
+                        reduce_w0(t - 1);   // wave 0's lanes of step t - 1
+                        if (tid == 64) tie_check<D, GF>(a, gsc, sc->row, t - 1, r0, r1, kNW);
+                    }
                 }
                 rescan_rest(t);
             }
@@ -1427,9 +1483,12 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             if (wid == 0) rescan_w0();
             __syncthreads();
         }
-        if (wid == 1 && done == a.m + 1) reduce_w0(a.m - 1);
+        if (wid == 1 && done == a.m + 1) {
+            if constexpr (kLanes) tie_check_lanes<D, GF, NT>(a, gsc, gl, sc->row, a.m - 1, r0, r1);
+            else reduce_w0(a.m - 1);
+        }
         if (tid == 64 && done == a.m + 1) {
-            tie_check<D, GF>(a, gsc, sc->row, a.m - 1, r0, r1, kNW);
+            if constexpr (!kLanes) tie_check<D, GF>(a, gsc, sc->row, a.m - 1, r0, r1, kNW);
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)
                 double* st_out = const_cast<double*>(a.tie_bounds) + 2;
                 st_out[0] = gsc->tg[3];

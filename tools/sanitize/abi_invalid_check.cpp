@@ -80,6 +80,16 @@ int main() {
     EXPECT_ERR(st_kmat(p, p, nullptr, 100, 64, 4, 1.0, 4.0, p, nullptr));
     EXPECT_ERR(st_layout_soa(nullptr, 10, 4, 64, p, nullptr));
     EXPECT_ERR(st_layout_soa(p, 10, 4, 5, p, nullptr));
+    // round 5: the device-tensor download, the near-tie flag read-back, the tuning read-back
+    int32_t st5 = 0;
+    int64_t step5 = 0;
+    EXPECT_ERR(st_standardize_download(nullptr, 100, 4, p, p, p, &st5, nullptr));
+    EXPECT_ERR(st_standardize_download(p, 0, 4, p, p, p, &st5, nullptr));
+    EXPECT_ERR(st_standardize_download(p, 100, 4, p, p, p, nullptr, nullptr));
+    EXPECT_ERR(st_greedy_near_tie(nullptr, 4096, &step5, nullptr));
+    EXPECT_ERR(st_greedy_near_tie(p, 64, &step5, nullptr));
+    EXPECT(st_tune_get(20) == 0 || st_tune_get(20) == 1);
+    EXPECT(st_tune_get(12345) < 0);
     // energy distance
     EXPECT_ERR(st_distance_colsum(nullptr, 64, 10, p, 64, 10, 4, 0, 10, 0, p, nullptr));
     EXPECT_ERR(st_distance_colsum(p, 64, 10, p, 64, 10, 4, 5, 11, 0, p, nullptr));
