@@ -63,8 +63,8 @@ struct Scratch {          // small per-block scratch at the start of the dynamic
 
 // near-tie guard state (GUARD kernels only: after Scratch in the dynamic LDS), by step parity: the
 // rescan's per-wave minimum, its row and the wave's second-smallest sum; the step's winner (row and sum;
-// its score row and weight are read from Scratch::row, which holds them until the next pick) and this
-// block's published minimum; the threshold recurrence
+// tie_check reads its score row and weight from the inputs) and this block's published minimum; the
+// threshold recurrence
 struct GuardScratch {
     double rs_min[2][kMaxPWaves], rs_run[2][kMaxPWaves];
     uint32_t rs_idx[2][kMaxPWaves];
@@ -506,11 +506,17 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
         __hip_atomic_fetch_max(a.tie, ~(unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const double Q = ts[3] + v;
-    const double* gj = row + D;   // the winner's g (and w), in Scratch::row until the next pick
+    // the winner's g (and w) from the read-only inputs: Scratch::row may already hold the next step's
+    // winner (this check runs one step late, off the critical path, and the next pick does not wait)
+    (void)row;
+    const int64_t gr = (int64_t)gi < a.n ? (int64_t)gi : 0;   // a completed pick's row is always < n
+    double gj[D];
+#pragma unroll
+    for (int k = 0; k < D; ++k) gj[k] = a.g[(int64_t)k * a.ld + gr];
     double gj2 = gj[0] * gj[0];
 #pragma unroll
     for (int k = 1; k < D; ++k) gj2 = gj2 + gj[k] * gj[k];
-    const double wj = GF ? gj[D] : 1.0;
+    const double wj = GF ? a.w[gr] : 1.0;
     const double scale = (ts[0] + gj2) * (ts[1] * wj);
     const double E = ts[4] + (16.0 * scale + (2.0 * ts[2] + __builtin_fmax(Q, 0.0)));
     ts[3] = Q;
