@@ -159,3 +159,21 @@ def test_dropin_equals_numpy_on_near_ties_at_scale(n):
     _, _, _, _, flagged = oc.greedy_ties(integrand.sample, integrand.gradient, None, integrand.linv_scale,
                                          integrand.linv_trace, 20)
     assert step == np.flatnonzero(flagged)[0]
+
+
+@pytest.mark.parametrize('n', [60, 300, 700, 5000])
+def test_kernel_state_on_few_blocks_long_runs(n):
+    """One to twenty blocks and up to 300 steps: the exchange is at its fastest, so the next pick lands
+    soonest after the late check of the previous step -- the check must read only step-parity state (the
+    winner's index and sum, the rescans) and the inputs.  Final (Q, E, thr) bit for bit against the model."""
+    X, G, _ = mr.near_tie_twins(4, n=n)
+    integrand = st._make_stein_integrand(X, G)
+    m = min(300, X.shape[0])
+    idx, step, state = _compact_run(integrand.device_problem(), m)
+    midx, _, _, _, flagged, wv = oc.greedy_ties(integrand.sample, integrand.gradient, None, integrand.linv_scale,
+                                                integrand.linv_trace, m, winner_sums=True)
+    np.testing.assert_array_equal(idx, midx)
+    assert step == (np.flatnonzero(flagged)[0] if flagged.any() else -1)
+    thr_all, Q, E = model_thresholds(integrand.gradient, None, integrand.linv_scale, integrand.linv_trace, midx, wv)
+    g2, w2 = oc.tie_bounds(integrand.gradient, None)
+    np.testing.assert_array_equal(state, [g2, w2, Q, E, thr_all[-1]])
