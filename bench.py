@@ -308,22 +308,31 @@ def _set_guard(enabled) -> bool:
 
 
 def rank_local_ms(integrand, m: int, rank: int, world: int, reps: int = 3):
-    """ms per thin of this rank's shard ALONE on its GPU: the single-device persistent kernel over rows
-    shard_bounds(n, rank, world), no rank exchange (HIP events on the launch stream, median) -- T_local
-    of DESIGN.md section 5's cost model T(N) = T_local(n / N) + H(N) + X."""
+    """ms per thin of this rank's shard ALONE on its GPU: the persistent kernel the rank runs (the
+    single-device compact-only variant switched off) over rows shard_bounds(n, rank, world), no rank
+    exchange (HIP events on the launch stream, median) -- T_local of DESIGN.md section 5's cost model
+    T(N) = T_local(n / N) + H(N) + X."""
     import torch
     from stein_thinning import distributed as sd
+    from stein_thinning import _native as nat
     lo, hi = sd.shard_bounds(integrand.n, rank, world)
     prob = integrand.device_problem().subset(np.arange(lo, hi))
     idx, a, ws = prob.greedy_buffers(m)
-    prob.greedy_launch(m, idx, a, ws)
-    stream = torch.cuda.current_stream()
-    evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
-    for e0, e1 in evs:
-        e0.record(stream)
+    L = nat.lib()
+    prev = L.st_tune_get(12)
+    # the kernel a rank runs: the compact-only variant is single-device only (st_tune key 12 off here)
+    nat.check(L.st_tune(12, 0), 'st_tune')
+    try:
         prob.greedy_launch(m, idx, a, ws)
-        e1.record(stream)
-    torch.cuda.synchronize()
+        stream = torch.cuda.current_stream()
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for e0, e1 in evs:
+            e0.record(stream)
+            prob.greedy_launch(m, idx, a, ws)
+            e1.record(stream)
+        torch.cuda.synchronize()
+    finally:
+        nat.check(L.st_tune(12, prev), 'st_tune')
     return float(np.median([e0.elapsed_time(e1) for e0, e1 in evs]))
 
 
