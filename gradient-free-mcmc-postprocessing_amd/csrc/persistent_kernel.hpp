@@ -472,8 +472,8 @@ __device__ __forceinline__ void top2_wave(GuardScratch* sc, const Top2& r, int p
 // (stein_ref.c tie_init / tie_step, the same operations).  Step 0 first reads the problem's bounds,
 // which every block merged before publishing step 0 (so this block's sweep of step 0 saw them all)
 template <int D, bool GF>
-__device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc, const double* row, int64_t t,
-                                          int64_t r0, int64_t r1, int nwaves) {
+__device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc, int64_t t, int64_t r0, int64_t r1,
+                                          int nwaves) {
     const int par = (int)(t & 1);
     double* ts = sc->tg;   // c1, wmax, Dmax, Q, E, thr
     if (t == 0) {   // stein_ref.c tie_init
@@ -508,7 +508,6 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
     const double Q = ts[3] + v;
     // the winner's g (and w) from the read-only inputs: Scratch::row may already hold the next step's
     // winner (this check runs one step late, off the critical path, and the next pick does not wait)
-    (void)row;
     const int64_t gr = (int64_t)gi < a.n ? (int64_t)gi : 0;   // a completed pick's row is always < n
     double gj[D];
 #pragma unroll
@@ -529,7 +528,7 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
 // other blocks only compare their published minimum; then lane 0 runs tie_check on that one slot
 template <int D, bool GF, int NT>
 __device__ __forceinline__ void tie_check_lanes(const PersistArgs& a, GuardScratch* sc, const GuardLanes* gl,
-                                                const double* row, int64_t t, int64_t r0, int64_t r1) {
+                                                int64_t t, int64_t r0, int64_t r1) {
     static_assert(NT <= 256, "GuardLanes holds 256 threads");
     const int par = (int)(t & 1);
     const uint32_t gi = sc->win_i[par];
@@ -539,7 +538,7 @@ __device__ __forceinline__ void tie_check_lanes(const PersistArgs& a, GuardScrat
         for (int k = (int)(threadIdx.x & 63); k < NT; k += 64) r.merge(gl->b[par][k], gl->b2[par][k], gl->bi[par][k]);
         top2_wave(sc, r, par, 0);
     }
-    if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, row, t, r0, r1, 1);
+    if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, t, r0, r1, 1);
 }
 
 // wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
@@ -1465,10 +1464,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             if (wid >= 1) {   // off the critical path: these waves only wait for the sweep now
                 if (wid == 1) {
                     if constexpr (kLanes) {
-                        tie_check_lanes<D, GF, NT>(a, gsc, gl, sc->row, t - 1, r0, r1);
+                        tie_check_lanes<D, GF, NT>(a, gsc, gl, t - 1, r0, r1);
                     } else {
                         reduce_w0(t - 1);   // wave 0's lanes of step t - 1
-                        if (tid == 64) tie_check<D, GF>(a, gsc, sc->row, t - 1, r0, r1, kNW);
+                        if (tid == 64) tie_check<D, GF>(a, gsc, t - 1, r0, r1, kNW);
                     }
                 }
                 rescan_rest(t);
@@ -1490,11 +1489,11 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             __syncthreads();
         }
         if (wid == 1 && done == a.m + 1) {
-            if constexpr (kLanes) tie_check_lanes<D, GF, NT>(a, gsc, gl, sc->row, a.m - 1, r0, r1);
+            if constexpr (kLanes) tie_check_lanes<D, GF, NT>(a, gsc, gl, a.m - 1, r0, r1);
             else reduce_w0(a.m - 1);
         }
         if (tid == 64 && done == a.m + 1) {
-            if constexpr (!kLanes) tie_check<D, GF>(a, gsc, sc->row, a.m - 1, r0, r1, kNW);
+            if constexpr (!kLanes) tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW);
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)
                 double* st_out = const_cast<double*>(a.tie_bounds) + 2;
                 st_out[0] = gsc->tg[3];
