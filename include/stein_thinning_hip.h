@@ -57,8 +57,9 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * Kernel-variant tuning (process-wide, host side; for measurement sweeps -- defaults are the
  * measured best on MI355X): key 0 = grid cap (blocks, 1..1024), key 1 = candidates per lane
  * (1, 2, 4; d = 2 and 4 kernels; -1 = automatic), key 2 = register prefetch of the next tile
- * (0/1; -1 = automatic), key 3 = persistent kernel register rows per thread (4, 8, 16;
- * -1 = automatic, 0 = disable the persistent kernel), key 4 = persistent kernel threads per
+ * (0/1; -1 = automatic), key 3 = persistent kernel register rows per thread (4, 8, 16; 1, 2 on
+ * 256-thread blocks whose rows they hold; -1 = automatic: 1 / 2 for blocks of at most 256 / 512 rows,
+ * else the fewest of 16 / 8 / 4 without empty rows; 0 = disable the persistent kernel), key 4 = persistent kernel threads per
  * block (256, 512; -1 = automatic: 512 with dynamic chunks above 1280 rows per block), key 5 = persistent kernel grid cap (blocks per device,
  * 1..256; -1 = one per CU), key 6 = grid cap of the d > 8 step kernel (1..1024), key 7 = proxy
  * kernel (0 = automatic: matrix cores for 16 < d <= 64; 1 = always the VALU kernel), key 8 =
