@@ -252,13 +252,15 @@ def check(rc: int, what: str = '') -> None:
         raise HipExtensionError(f'{what}: HIP error ({rc}): {msg}')
 
 
-def select_device_index(count: int, env=None, worker: bool = False, pid: int = 0):
+def select_device_index(count: int, env=None, worker: bool = False, pid: int = 0, worker_name: str = ''):
     """The device policy of a process (pure: tests call it with a mocked device count):
     * ``ST_DEVICE`` in the environment: that device (an index < count);
     * else ``LOCAL_RANK`` (torchrun / torch.distributed.run: one process per GPU): LOCAL_RANK % count;
     * else, in a worker process of a pool (joblib / loky / multiprocessing / Dask -- the reference fans
       ``thin`` out over chains in such workers, ``code/src/utils/parallel.py:48-52``) with several
-      devices: pid % count, so that consecutive workers land on different GPUs;
+      devices: the worker's ordinal from its process name ("LokyProcess-3", "ForkPoolWorker-3",
+      "SpawnProcess-3": (3 - 1) % count -- the pool's workers round-robin over the GPUs), or its
+      pid % count when the name carries none;
     * else None: the current torch device (cuda:0 unless the caller chose another).
     Returns the device index or None."""
     env = os.environ if env is None else env
@@ -275,7 +277,9 @@ def select_device_index(count: int, env=None, worker: bool = False, pid: int = 0
     if v is not None and v != '' and count > 0:
         return int(v) % count
     if worker and count > 1:
-        return pid % count
+        import re
+        k = re.search(r'-(\d+)$', worker_name or '')
+        return (int(k.group(1)) - 1) % count if k else pid % count
     return None
 
 
@@ -300,7 +304,9 @@ def require_device():
     global _DEVICE_POLICY_DONE
     if not _DEVICE_POLICY_DONE:
         _DEVICE_POLICY_DONE = True
-        idx = select_device_index(torch.cuda.device_count(), os.environ, _pool_worker(), os.getpid())
+        import multiprocessing
+        idx = select_device_index(torch.cuda.device_count(), os.environ, _pool_worker(), os.getpid(),
+                                  multiprocessing.current_process().name)
         if idx is not None and idx != torch.cuda.current_device():
             torch.cuda.set_device(idx)
     return torch.device('cuda', torch.cuda.current_device())

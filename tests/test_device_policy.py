@@ -25,6 +25,11 @@ def test_pool_workers_spread_round_robin():
     # five joblib workers (the reference's five chains) with consecutive pids on an 8-GPU node
     got = [nat.select_device_index(8, {}, worker=True, pid=4000 + k) for k in range(5)]
     assert len(set(got)) == 5
+    # the pool's own worker ordinals (loky / multiprocessing names): an exact round-robin
+    names = [f'LokyProcess-{k}' for k in range(1, 6)]
+    assert [nat.select_device_index(8, {}, worker=True, pid=9, worker_name=nm) for nm in names] == [0, 1, 2, 3, 4]
+    assert nat.select_device_index(4, {}, worker=True, pid=9, worker_name='ForkPoolWorker-6') == 1
+    assert nat.select_device_index(4, {}, worker=True, pid=9, worker_name='Dask worker') == 1   # pid 9 % 4
     assert nat.select_device_index(1, {}, worker=True, pid=4001) is None   # one device: nothing to choose
     assert nat.select_device_index(8, {}, worker=False, pid=4001) is None  # the main process: current device
 
