@@ -3,6 +3,7 @@
 # every bench workload's dominant kernel; summarised per launch into profiles/pmc_traffic.json by
 # tools/summarize_pmc.py (gfx950 FETCH_SIZE x2 correction).  Any failing pass ends the script.
 #   bash scripts/pmc_workloads.sh [key ...]      keys: energy ksd_c2 proxy_gauss proxy_t lv lv2 c4_persistent chains_batch
+#                                                 c4_dropin (the guarded thin of config 4's run starts)
 # PMC_SOURCE (environment) labels the records (round, commit).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -11,12 +12,12 @@ export TMPDIR=/tmp
 declare -A ARGS=( [energy]="--workload energy" [ksd_c2]="--workload ksd" [proxy_gauss]="--workload proxy"
                   [proxy_t]="--workload proxy --proxy-kind t" [lv]="--workload lv"
                   [c4_persistent]="--config c4 --no-kernel-timing" [lv2]="--workload lv"
-                  [chains_batch]="--workload chains" )
+                  [chains_batch]="--workload chains" [c4_dropin]="--config c4 --no-kernel-timing" )
 declare -A KERN=( [energy]="dist_colsum_kernel" [ksd_c2]="ksd_colsum_kernel" [proxy_gauss]="proxy_mfma_buf_kernel"
                   [proxy_t]="proxy_mfma_buf_kernel" [lv]="lv_kernel<10>"
                   [c4_persistent]="greedy_persistent<4, false, 9, 512, 1, true, false, st::PersistArgs, false>" [lv2]="lv_dense_kernel"
-                  [chains_batch]="st::BatchArgs, " )
-declare -A EXCL=( [c4_persistent]="@none@" [lv2]="@none@" [chains_batch]="@none@" )
+                  [chains_batch]="st::BatchArgs, " [c4_dropin]="greedy_persistent<4, false, 4, 512, 1, true, true, st::PersistArgs, true>" )
+declare -A EXCL=( [c4_persistent]="@none@" [lv2]="@none@" [chains_batch]="@none@" [c4_dropin]="@none@" )
 KEYS=("$@")
 [[ ${#KEYS[@]} -gt 0 ]] || KEYS=(energy ksd_c2 proxy_gauss proxy_t lv)
 for key in "${KEYS[@]}"; do
