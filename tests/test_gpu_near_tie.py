@@ -177,3 +177,22 @@ def test_kernel_state_on_few_blocks_long_runs(n):
     thr_all, Q, E = model_thresholds(integrand.gradient, None, integrand.linv_scale, integrand.linv_trace, midx, wv)
     g2, w2 = oc.tie_bounds(integrand.gradient, None)
     np.testing.assert_array_equal(state, [g2, w2, Q, E, thr_all[-1]])
+
+
+@pytest.mark.parametrize('seed', range(5))
+def test_dropin_thin_gf_equals_numpy_on_near_ties(seed):
+    """The gradient-free operator (weights w_i w_j in every pair and in the guard's bound): the twins of the
+    rows NumPy selects, with their own log densities; the default thin_gf returns NumPy's indices."""
+    X, G, steps = mr.near_tie_twins(seed)
+    cov = np.array([[1, .8], [.8, 1]])
+    log_p = -0.5 * np.sum(X * np.linalg.solve(cov, X.T).T, axis=1)
+    log_q = 0.9 * log_p   # a proxy close enough that the weights' spread stays under the warning
+    want = o.thin_gf(X, log_p, log_q, G, 30)
+    np.testing.assert_array_equal(stein_thinning.thin_gf(X, log_p, log_q, G, 30), want)
+    integrand = st._make_stein_gf_integrand(X, log_p, log_q, G)
+    np.testing.assert_array_equal(st._greedy_search(30, integrand), want)
+    assert integrand.device_problem().near_tie is not None and integrand.device_problem().near_tie >= -1
+    _, step, _ = _compact_run(integrand.device_problem(), 30)
+    _, _, _, _, flagged = oc.greedy_ties(integrand.sample, integrand.gradient, integrand.weights,
+                                         integrand.linv_scale, integrand.linv_trace, 30)
+    assert step == (np.flatnonzero(flagged)[0] if flagged.any() else -1)
