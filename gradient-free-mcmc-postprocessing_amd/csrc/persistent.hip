@@ -14,6 +14,8 @@ namespace st {
 const void* guarded_persistent_fn(int d, bool gf, int rt, int nt, int bpc, bool gen, bool batch);
 // the small-shard instantiations (persistent_small.hip: 256 threads, 1 / 2 register rows), or nullptr
 const void* small_persistent_fn(int d, bool gf, int rt, bool cmp, bool batch, bool guard);
+// the mid-size compact-only instantiations (persistent_cmp.hip: 512 threads, 4 / 6 register rows), or nullptr
+const void* cmp_persistent_fn(int d, bool gf, int rt, bool batch, bool guard);
 
 int64_t persistent_rep_stride(int G, int rec_stride, int nrep) {
     const int64_t one = (int64_t)G * rec_stride;
@@ -45,7 +47,7 @@ static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (on
 static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
 static int g_persist_pitch = -1; // st_tune key 9: record pitch in bytes (16 .. 4096, power of 2), -1 auto
 static int g_persist_nrep = -1;  // st_tune key 10: record replicas (1 .. 32, power of 2), -1 auto
-static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register rows (8 .. 10), 0 off, -1 auto
+static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register rows (4, 6, 8 .. 10), 0 off, -1 auto
 // st_tune key 15: the 512-thread kernels keep the streamed rows' running sums in LDS (1) or in HBM (0,
 // the default).  Measured (round 4, same box, config 4, profiles/r04_streamed_sums_lds_rejected.log):
 // PMC WRITE_SIZE 1.08 GB -> 0.15 GB per thin, but 6.82 -> 6.94-7.01 ms: the 8 B per streamed row take
@@ -127,7 +129,7 @@ int persistent_tune(int key, int value) {
         return 0;
     }
     if (key == 12) {
-        if (value != -1 && value != 0 && (value < 8 || value > 10)) return -1;
+        if (value != -1 && value != 0 && value != 4 && value != 6 && (value < 8 || value > 10)) return -1;
         g_persist_cmp = value;
         return 0;
     }
@@ -162,6 +164,10 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     if constexpr (RT < 4 && D <= kMaxCtDim) {   // small shards: compiled in persistent_small.hip
         static_assert(NT == 256 && BPC == 1 && GEN, "small-shard plans only");
         fn = small_persistent_fn(D, GF, RT, arith_compact(), b != nullptr, guarded);
+        if (!fn) return hipErrorNotSupported;
+    } else if constexpr (!GEN && RT < 8) {   // mid-size compact-only: compiled in persistent_cmp.hip
+        static_assert(NT == 512 && BPC == 1, "mid-size compact-only plans only");
+        fn = cmp_persistent_fn(D, GF, RT, b != nullptr, guarded);
         if (!fn) return hipErrorNotSupported;
     } else if (guarded) {
         if constexpr (D <= kMaxCtDim) {
@@ -210,12 +216,14 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     return hipLaunchKernel(fn, dim3(G), dim3(NT), kargs, lds, s);
 }
 
-// compact-only kernels: 512-thread blocks, 8 / 9 / 10 register rows per thread
+// compact-only kernels: 512-thread blocks, 4 / 6 / 8 / 9 / 10 register rows per thread
 template <int D, bool GF>
 static hipError_t launch_p_cmp(const PersistArgs& a, int rt, int G, size_t lds, hipStream_t s, bool dry,
                                const BatchArgs* b) {
     if (rt >= 10) return launch_p<D, GF, 10, 512, 1, false>(a, G, lds, s, dry, b);
     if (rt == 9) return launch_p<D, GF, 9, 512, 1, false>(a, G, lds, s, dry, b);
+    if (rt <= 4) return launch_p<D, GF, 4, 512, 1, false>(a, G, lds, s, dry, b);
+    if (rt <= 6) return launch_p<D, GF, 6, 512, 1, false>(a, G, lds, s, dry, b);
     return launch_p<D, GF, 8, 512, 1, false>(a, G, lds, s, dry, b);
 }
 
@@ -274,7 +282,8 @@ struct Plan {
 static hipError_t plan_persistent(const double* x, const double* g, const double* w, double* A, int64_t n,
                                   int d, int64_t ld, double l, double tr, int64_t m, uint32_t* idx_out,
                                   void* ws, int64_t ws_bytes, hipStream_t s, int* used, const RankSpec* rs,
-                                  bool plan_only, int grid_cap, Plan& P, int rt_force = 0) {
+                                  bool plan_only, int grid_cap, Plan& P, int rt_force = 0,
+                                  int cmp_force = 0, bool batch = false) {
     const RankSpec one{0, n, 0, 1, 0, nullptr, {}};
     if (!rs) rs = &one;
     // 32-bit row indices, padding rows included (< n + one block's register rows)
@@ -408,17 +417,27 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     bool use_cmp = false;
     int rt_c = 0;
     size_t lds_c = 0;
+    // (round 5: a single launch from 1 280 rows per block, every 512-thread plan -- below 8 x 512 rows with
+    // the fewest of 4 / 6 / 8 register rows that hold the block, where the general kernel keeps 4 and the
+    // rest in LDS: the LV call -1 %; a batch of such blocks ran 5 % slower than the general kernel's, so a
+    // batch keeps the 8 x 512 floor -- profiles/r05_mid_compact_ab.log)
     if (rs->nranks == 1 && arith_compact() && nt == 512 && bpc == 1 && !wide && g_persist_cmp != 0 &&
-        R >= 8 * 512) {
+        (!batch || R >= 8 * 512 || cmp_force > 0 || g_persist_cmp > 0)) {
         const int64_t rl_cap = (int64_t)((budget - head) / row_bytes) / 64 * 64;
-        rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R - 9 * 512 - rl_cap > kCmpStreamRows ? 10 : 9);
-        while (rt_c > 8 && (int64_t)rt_c * 512 > R) --rt_c;   // no empty register rows
+        if (cmp_force > 0)
+            rt_c = cmp_force;   // a batch's common register rows (launch_greedy_persistent_batch)
+        else if (R >= 8 * 512)
+            rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R - 9 * 512 - rl_cap > kCmpStreamRows ? 10 : 9);
+        else
+            rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R <= 4 * 512 ? 4 : (R <= 6 * 512 ? 6 : 8));
+        while (cmp_force <= 0 && rt_c > 8 && (int64_t)rt_c * 512 > R) --rt_c;   // no empty register rows
         int64_t RLc = 0;
         int salc = 0;
         lds_rows(512, rt_c, RLc, lds_c, salc);
         ac.RL = (int)RLc;
         ac.stream_a_lds = salc;
-        ac.poll_delay = g_persist_delay >= 0 ? g_persist_delay : 10;
+        // (the first-poll delay pays only at the headline's 2e6 rows: r04_first_poll_delay.log, r05_knobs_recheck.log)
+        ac.poll_delay = g_persist_delay >= 0 ? g_persist_delay : (R >= 8 * 512 ? 10 : 0);
         use_cmp = offsets_ok(512, rt_c, RLc) &&
                   launch_cmp(ac, d, gf, rt_c, G, lds_c, s, true) == hipSuccess;   // residency check only
     }
@@ -494,29 +513,34 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
     bc.count = bg.count = count;
     size_t lds = 0, lds_c = 0;
     // plans that differ only in the small-shard register rows (256 threads, 1 / 2 / 4 rows per thread)
-    // are planned again with the largest of them: one kernel for the batch
-    int rt_force = 0;
+    // or in the compact-only kernel's register rows are planned again with the largest of them: one
+    // kernel for the batch
+    int rt_force = 0, cmp_force = 0;
     for (int attempt = 0; attempt < 2; ++attempt) {
         bool rt_only = true;
-        int rt_max_seen = 0;
+        int rt_max_seen = 0, rtc_max_seen = 0;
         for (int q = 0; q < count; ++q) {
             int u = 0;
             hipError_t e = plan_persistent(pr[q].x, pr[q].g, pr[q].w, pr[q].A, pr[q].n, d, pr[q].ld, pr[q].l,
                                            pr[q].tr, m, pr[q].idx_out, pr[q].ws, pr[q].ws_bytes, s, &u, nullptr, false,
-                                           cap, P[q], rt_force);
+                                           cap, P[q], rt_force, cmp_force, true);
             if (e != hipSuccess) return e;
             const Plan& p0 = P[0];
-            if (P[q].wide || P[q].nt != p0.nt || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].use_cmp != p0.use_cmp ||
-                (p0.use_cmp && P[q].rt_c != p0.rt_c))
+            if (P[q].wide || P[q].nt != p0.nt || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].use_cmp != p0.use_cmp)
                 return hipErrorNotSupported;
             rt_max_seen = std::max(rt_max_seen, P[q].rt);
+            rtc_max_seen = std::max(rtc_max_seen, P[q].rt_c);
             if (P[q].rt != p0.rt && !(P[q].nt == 256 && P[q].rt <= 4 && p0.rt <= 4)) rt_only = false;
         }
-        bool same = true;
-        for (int q = 1; q < count; ++q) same &= P[q].rt == P[0].rt;
-        if (same) break;
+        bool same_rt = true, same_c = true;
+        for (int q = 1; q < count; ++q) {
+            same_rt &= P[q].rt == P[0].rt;
+            same_c &= P[q].rt_c == P[0].rt_c;
+        }
+        if (same_rt && same_c) break;
         if (!rt_only || attempt == 1) return hipErrorNotSupported;
-        rt_force = rt_max_seen;
+        if (!same_rt) rt_force = rt_max_seen;
+        if (!same_c) cmp_force = rtc_max_seen;
     }
     for (int q = 0; q < count; ++q) {
         P[q].a.stamps = P[q].ac.stamps = nullptr;

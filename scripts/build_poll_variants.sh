@@ -9,7 +9,7 @@ HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 FL="--offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -Wall"
 for ps in "$@"; do
   D=tools/ab/ps$ps; mkdir -p $D/obj
-  for f in persistent persistent_guard persistent_small; do
+  for f in persistent persistent_guard persistent_small persistent_cmp; do
     $HIPCC $FL -DST_POLL_SYNC=$ps -c -o $D/obj/$f.o $CS/$f.hip &
   done
 done
@@ -17,7 +17,7 @@ wait
 for ps in "$@"; do
   D=tools/ab/ps$ps
   $HIPCC --offload-arch=gfx950 -fPIC -shared -o $D/libstein_hip.so $O/capi.o $O/dedup.o $O/precon.o $O/greedy.o \
-    $D/obj/persistent.o $D/obj/persistent_guard.o $D/obj/persistent_small.o $O/pairwise.o $O/proxy.o $O/kde.o $O/lv.o \
+    $D/obj/persistent.o $D/obj/persistent_guard.o $D/obj/persistent_small.o $D/obj/persistent_cmp.o $O/pairwise.o $O/proxy.o $O/kde.o $O/lv.o \
     $O/host_prep.o $O/prep_upload.o
   rm -rf $D/obj
 done

@@ -11,7 +11,7 @@ $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -o tools/probe tools/probe.hip -L$LI
 mkdir -p tools/_diag
 $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fPIC -shared -DST_PERSIST_STAMPS \
   -o tools/_diag/libstein_hip.so $CS/capi.hip $CS/dedup.hip $CS/precon.hip $CS/greedy.hip $CS/persistent.hip \
-  $CS/persistent_guard.hip $CS/persistent_small.hip $CS/pairwise.hip $CS/proxy.hip $CS/kde.hip $CS/lv.hip $CS/host_prep.cpp $CS/prep_upload.cpp
+  $CS/persistent_guard.hip $CS/persistent_small.hip $CS/persistent_cmp.hip $CS/pairwise.hip $CS/proxy.hip $CS/kde.hip $CS/lv.hip $CS/host_prep.cpp $CS/prep_upload.cpp
 $HIPCC --offload-arch=gfx950 -O3 -std=c++17 -DST_PERSIST_STAMPS -o tools/_diag/probe_stamps tools/probe.hip \
   -Ltools/_diag -lstein_hip -Wl,-rpath,'$ORIGIN'
 echo built
