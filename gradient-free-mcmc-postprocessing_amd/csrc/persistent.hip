@@ -419,8 +419,8 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     size_t lds_c = 0;
     // (round 5: a single launch from 1 280 rows per block, every 512-thread plan -- below 8 x 512 rows with
     // the fewest of 4 / 6 / 8 register rows that hold the block, where the general kernel keeps 4 and the
-    // rest in LDS: the LV call -1 %; a batch of such blocks ran 5 % slower than the general kernel's, so a
-    // batch keeps the 8 x 512 floor -- profiles/r05_mid_compact_ab.log)
+    // rest in LDS: the LV call -1 %; a batch of such blocks gained nothing (the LV chains: within noise,
+    // 5 % slower in a first A/B), so a batch keeps the 8 x 512 floor -- profiles/r05_mid_compact_ab.log)
     if (rs->nranks == 1 && arith_compact() && nt == 512 && bpc == 1 && !wide && g_persist_cmp != 0 &&
         (!batch || R >= 8 * 512 || cmp_force > 0 || g_persist_cmp > 0)) {
         const int64_t rl_cap = (int64_t)((budget - head) / row_bytes) / 64 * 64;
