@@ -418,8 +418,7 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     int rt_c = 0;
     size_t lds_c = 0;
     // (round 5: a single launch from 1 280 rows per block, every 512-thread plan -- below 8 x 512 rows with
-    // the fewest of 4 / 6 / 8 register rows that hold the block, where the general kernel keeps 4 and the
-    // rest in LDS: the LV call -1 %; a batch of such blocks gained nothing (the LV chains: within noise,
+    // 4 or 6 register rows, where the general kernel keeps 4 and the rest in LDS: the LV call -1 %; a batch of such blocks gained nothing (the LV chains: within noise,
     // 5 % slower in a first A/B), so a batch keeps the 8 x 512 floor -- profiles/r05_mid_compact_ab.log)
     if (rs->nranks == 1 && arith_compact() && nt == 512 && bpc == 1 && !wide && g_persist_cmp != 0 &&
         (!batch || R >= 8 * 512 || cmp_force > 0 || g_persist_cmp > 0)) {
@@ -429,7 +428,9 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
         else if (R >= 8 * 512)
             rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R - 9 * 512 - rl_cap > kCmpStreamRows ? 10 : 9);
         else
-            rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R <= 4 * 512 ? 4 : (R <= 6 * 512 ? 6 : 8));
+            // empty register slots are swept like full ones, LDS rows cost ~1.7 register rows: 4 up to
+            // 5 x 512 rows, then 6 (profiles/r05_mid_rows_probe.log: 8 never won below 8 x 512)
+            rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R <= 5 * 512 ? 4 : 6);
         while (cmp_force <= 0 && rt_c > 8 && (int64_t)rt_c * 512 > R) --rt_c;   // no empty register rows
         int64_t RLc = 0;
         int salc = 0;

@@ -1,9 +1,9 @@
-// Compact-only instantiations of the persistent greedy kernel for mid-size blocks: 512 threads with FOUR or
-// SIX register rows per thread (1 280 .. 3 072 rows per block: config 4's run starts, the LV call's 5e5 rows,
-// the chains of a batch launch), plain, batch and guarded.  The compact-only kernel carries no exact /
-// mixed sweep, so it holds every row of such a block in registers where the general kernel of the same
-// plan keeps four rows per thread and the rest in LDS.  A translation unit of their own, compiled in
-// parallel with persistent.hip.
+// Compact-only instantiations of the persistent greedy kernel for mid-size blocks: 512 threads with FOUR
+// or SIX register rows per thread and the rest of the block in LDS (1 280 .. 4 095 rows per block on a
+// single launch: config 4's run starts, the LV call's 5e5 rows), plain, batch and guarded.  The
+// compact-only kernel carries no exact / mixed sweep, so it runs leaner than the general kernel of the
+// same rows (profiles/r05_mid_rows_probe.log).  A translation unit of their own, compiled in parallel
+// with persistent.hip.
 #include "persistent_kernel.hpp"
 
 namespace st {

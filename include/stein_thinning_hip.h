@@ -74,7 +74,7 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * oracle/stein_ref.c and DESIGN.md §3; all ranks of a sharded run must use the same value), key 12 =
  * register rows per thread of the one-device compact-only persistent kernel (4, 6, 8 .. 10; 0 = do
  * not use it; -1 = automatic: from 8 x 512 rows per block 9, or 10 when more than 2048 rows per block
- * would still be streamed; below that the fewest of 4 / 6 / 8 that hold the block), key 13 = energy-distance kernel variant (0 / -1 = automatic = 1:
+ * would still be streamed; below that 4 up to 2 560 rows per block, else 6), key 13 = energy-distance kernel variant (0 / -1 = automatic = 1:
  * one partial sum per thread, 4 blocks per CU; 2..5: more partial sums or 8 blocks per CU; 6: the
  * round-2 zero-distance select -- measured alternatives; same distances, sums within
  * rounding), key 14 = energy-distance work units: grid blocks (256 columns x one B chunk) that
