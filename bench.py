@@ -184,19 +184,16 @@ def make_integrand(cfg):
 
 def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None, arith='compact'):
     """Host baselines on the same standardised input (test-infrastructure code, timed only):
-    * primary: the C restatement (oracle/stein_ref.c sr_greedy_mt -- the kernels' bit model, rows
-      split over host threads like the reference's process fan-out, code/src/utils/parallel.py:48-52)
-      running the FULL m-step thin on the box's CPU share; its indices are compared with the GPU's;
-    * `numpy_1core`: the NumPy restatement of the reference path (oracle/stein_numpy.py: the
-      (d, n) transposed vfk0_imq, A += 2 col, np.argmin) for the diagonal + `steps` steps on one
-      core (NumPy ufuncs are single-threaded), extrapolated to m."""
+    * primary (`value`): the NumPy restatement of the reference path (oracle/stein_numpy.py: the (d, n)
+      transposed vfk0_imq, A += 2 col, np.argmin -- JAX_Stein_Thinning.ipynb:281-295, 354-361) for the
+      diagonal + `steps` steps on one core (NumPy ufuncs are single-threaded), its rate extrapolated
+      linearly in m (every step costs the same n pair-evaluations);
+    * `c_port`: the C restatement (oracle/stein_ref.c sr_greedy_mt -- the kernels' bit model, rows split
+      over host threads like the reference's process fan-out, code/src/utils/parallel.py:48-52) running the
+      FULL m-step thin on the box's CPU share; its indices are compared with the GPU's."""
     from oracle import stein_numpy as ref
     from oracle import stein_ref_c
     s, g, w = integrand.sample, integrand.gradient, integrand.weights
-    nt = stein_ref_c.host_threads()
-    t0 = time.perf_counter()
-    cidx, _ = stein_ref_c.greedy_mt(s, g, w, integrand.linv_scale, integrand.linv_trace, cfg['m'], nt, arith=arith)
-    dt_c = time.perf_counter() - t0
     vfk0 = ref.make_imq(s, 'med')
     if w is None:
         def f(i1, i2):
@@ -204,25 +201,32 @@ def cpu_baseline(cfg, integrand, steps: int, gpu_idx=None, arith='compact'):
     else:
         def f(i1, i2):
             return vfk0(s[i1], s[i2], g[i1], g[i2]) * w[i1] * w[i2]
+    steps = min(steps, cfg['m'] - 1)
     t0 = time.perf_counter()
-    ref._greedy_search(steps + 1, f)
+    np_idx = ref._greedy_search(steps + 1, f)
     dt = time.perf_counter() - t0
     pairs = cfg['n'] * (steps + 1)
     full = cfg['n'] * cfg['m']
+    nt = stein_ref_c.host_threads()
+    t0 = time.perf_counter()
+    cidx, _ = stein_ref_c.greedy_mt(s, g, w, integrand.linv_scale, integrand.linv_trace, cfg['m'], nt, arith=arith)
+    dt_c = time.perf_counter() - t0
     host = f"{platform.processor() or platform.machine()} ({os.cpu_count()} logical CPUs visible)"
     share = ('the box\'s CPU share for its one GPU: the pool sets OMP_NUM_THREADS=16 and allows '
              '16 CPUs per GPU, while os.cpu_count() reports the whole host' if os.environ.get('OMP_NUM_THREADS') == '16'
              else f'OMP_NUM_THREADS / os.cpu_count() on this host')
-    return {'value': full / dt_c, 'unit': 'pair-evals/s', 'cores': nt, 'cores_reason': share, 'kind': 'port',
-            'sample': (f"oracle/stein_ref.c sr_greedy_mt (C restatement of the reference greedy loop, "
-                       f"JAX_Stein_Thinning.ipynb:281-295, bit model of the kernels, {arith} arithmetic) on {nt} host "
-                       f"threads: the full "
-                       f"n={cfg['n']}, m={cfg['m']} thin ({full:.3g} pair-evals) in {dt_c:.1f} s; host {host}"),
-            'same_indices_as_gpu': None if gpu_idx is None else bool(np.array_equal(cidx, gpu_idx)),
-            'numpy_1core': {'value': pairs / dt, 'unit': 'pair-evals/s', 'cores': 1,
-                            'sample': (f"oracle.stein_numpy._greedy_search (NumPy restatement of the reference "
-                                       f"path), diagonal + {steps} steps = {pairs:.3g} pair-evals in {dt:.1f} s; "
-                                       f"full thin extrapolated {full * dt / pairs:.0f} s; NumPy {np.__version__}")}}
+    return {'value': pairs / dt, 'unit': 'pair-evals/s', 'cores': 1, 'kind': 'port',
+            'sample': (f"oracle.stein_numpy._greedy_search (NumPy restatement of the reference path, "
+                       f"JAX_Stein_Thinning.ipynb:281-295) on the same standardised sample: diagonal + {steps} steps "
+                       f"= {pairs:.3g} pair-evals in {dt:.1f} s on one core (NumPy ufuncs are single-threaded); the "
+                       f"full n={cfg['n']}, m={cfg['m']} thin extrapolated linearly: {full * dt / pairs:.0f} s; NumPy "
+                       f"{np.__version__}; host {host}"),
+            'same_indices_as_gpu_prefix': None if gpu_idx is None else bool(np.array_equal(np_idx, gpu_idx[:steps + 1])),
+            'c_port': {'value': full / dt_c, 'unit': 'pair-evals/s', 'cores': nt, 'cores_reason': share,
+                       'sample': (f"oracle/stein_ref.c sr_greedy_mt (C restatement of the reference greedy loop, "
+                                  f"the kernels' bit model, {arith} arithmetic) on {nt} host threads: the full "
+                                  f"thin ({full:.3g} pair-evals) in {dt_c:.1f} s"),
+                       'same_indices_as_gpu': None if gpu_idx is None else bool(np.array_equal(cidx, gpu_idx))}}
 
 
 def kernel_timing(prob, n_points: int, repeats: int = 5):
@@ -390,6 +394,91 @@ def config5_sharded(rank: int, world: int, dev, steps: int = 3):
                     f"({flop} flop per pair) per rank / the rank's launch median / {FP64_VALU_PEAK_TFS} TF"}
 
 
+def lv_chains(count: int, n: int, seed: int):
+    """`count` RW-MH surrogate chains of n rows each in the reference's LV call shape ('exp', lv_call_shape),
+    generated side by side (one vectorised lv_surrogate pool, chain-major): [(sample, gradient), ...]."""
+    s, gs, _, _ = lv_surrogate(count * n, seed, chain_len=n)
+    out = []
+    for c in range(count):
+        sc, gc = s[c * n:(c + 1) * n], gs[c * n:(c + 1) * n]
+        theta = np.exp(sc)
+        out.append((theta, gc / theta))
+    return out
+
+
+def chains_over_gpus(rank: int, world: int, dev, chains: int = 5, reps: int = 3):
+    """The reference's own multi-device split: its notebook thins each of the 5 LV
+    chains (n ~ 5e5 -> m = 10 000, 'med', Stein_thinning.ipynb:202-204) in a worker per chain
+    (code/src/utils/parallel.py:48-52).  Here chain c goes to rank c % world; every rank thins its chains
+    with the drop-in path on its own GPU (device.greedy_concurrent: repeated rows dropped, near-tie guard
+    on, one batch launch per GPU).  Timed barrier to barrier, max over ranks, median of `reps`; beside it
+    ONE GPU thinning all the chains in one batch launch (rank 0 alone), and the indices of both compared
+    with the per-chain loop (rank 0: DeviceProblem.greedy one chain after the other).  Collective; nulls
+    at one rank."""
+    nulls = {'ms_per_chains': None, 'one_gpu_batch_ms': None, 'speedup_vs_one_gpu': None,
+             'same_indices_as_loop': None, 'note': 'measured only when bench.py runs on N > 1 ranks'}
+    if world == 1:
+        return nulls
+    import torch
+    import torch.distributed as dist
+    from stein_thinning import device as sdev
+    from stein_thinning import thinning as st
+    from stein_thinning import _native as nat
+    n, m = 500_000, 10_000
+    mine = [c for c in range(chains) if c % world == rank]
+    data = lv_chains(chains, n, 20_500) if rank == 0 else None
+    if rank != 0:   # the same chains on every rank (one seeded pool; generated where needed)
+        data = lv_chains(chains, n, 20_500) if mine else []
+    probs = {c: st._make_stein_integrand(*data[c], preconditioner='med').device_problem() for c in mine}
+    guard = nat.near_tie_guard()
+
+    def run_mine():
+        for p in probs.values():
+            p._dedup = False   # run detection inside the timed region
+        return sdev.greedy_concurrent([probs[c] for c in mine], m, dedup=True, guard=guard) if mine else []
+    got = dict(zip(mine, run_mine()))   # warm-up
+    times = []
+    for _ in range(reps):
+        dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        got = dict(zip(mine, run_mine()))
+        torch.cuda.synchronize()
+        times.append(time.perf_counter() - t0)
+        dist.barrier()
+    ms = _max_over_ranks([float(np.median(times)) * 1e3], dev)[0]
+    parts = [None] * world
+    dist.all_gather_object(parts, {c: v.tolist() for c, v in got.items()})
+    one_ms, same = None, None
+    if rank == 0:
+        allp = [probs[c] if c in probs else st._make_stein_integrand(*data[c], preconditioner='med').device_problem()
+                for c in range(chains)]
+        loop = [p.greedy(m, dedup=True, guard=guard) for p in allp]
+        one = []
+        for _ in range(2):
+            for p in allp:
+                p._dedup = False
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            batch_idx = sdev.greedy_concurrent(allp, m, dedup=True, guard=guard)
+            torch.cuda.synchronize()
+            one.append(time.perf_counter() - t0)
+        one_ms = float(np.median(one)) * 1e3
+        spread = {c: np.asarray(v, dtype=np.uint32) for part in parts for c, v in part.items()}
+        same = bool(all(np.array_equal(spread[c], loop[c]) and np.array_equal(batch_idx[c], loop[c])
+                        for c in range(chains)))
+    dist.barrier()
+    return {'ms_per_chains': round(ms, 3), 'one_gpu_batch_ms': round(one_ms, 3) if one_ms else None,
+            'speedup_vs_one_gpu': round(one_ms / ms, 3) if one_ms else None, 'chains': chains,
+            'chains_per_rank': [len([c for c in range(chains) if c % world == r]) for r in range(world)],
+            'n_per_chain': n, 'm': m, 'near_tie_guard': guard, 'same_indices_as_loop': same,
+            'note': 'the reference\'s fan-out (one chain per worker, code/src/utils/parallel.py:48-52): chain c on '
+                    'rank c % world, each GPU thinning its chains with the drop-in path (run starts, near-tie guard, '
+                    'one batch launch); ms = barrier to barrier, max over ranks; one_gpu_batch_ms = all chains in '
+                    'one batch launch on rank 0\'s GPU; indices of both against the per-chain loop' +
+                    (' -- ranks SHARE one GPU here (rehearsal)' if SHARE_DEVICE else '')}
+
+
 # Rehearsal mode (ST_BENCH_SHARE_DEVICE=1, never used by the driver): every rank on cuda:0 and a
 # gloo group, so the N > 1 flow (mailbox setup, device exchange, timing reductions) can run on a
 # one-GPU box with several processes sharing the device.
@@ -470,13 +559,15 @@ def main():
     ap.add_argument('--steps', type=int, default=5, help='timed thins')
     ap.add_argument('--warmup', type=int, default=2)
     ap.add_argument('--config', default='c4', choices=sorted(CONFIGS))
-    ap.add_argument('--cpu-steps', type=int, default=30, help='greedy steps of the NumPy one-core sample')
+    ap.add_argument('--cpu-steps', type=int, default=100, help='greedy steps of the NumPy one-core sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
     ap.add_argument('--no-graph', action='store_true', help='N > 1: eager per-step launches instead of a HIP graph')
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     ap.add_argument('--no-config5', action='store_true',
                     help='thin workload at N > 1: skip the config5_sharded object (config 5 row-sharded)')
+    ap.add_argument('--no-chains', action='store_true',
+                    help='thin workload at N > 1: skip the chains_over_gpus object (the 5 LV chains over the ranks)')
     ap.add_argument('--ksd-full', action='store_true', help='ksd workload on config 4 (n = 2e6) instead of config 2')
     ap.add_argument('--proxy-kind', default='gauss', choices=['gauss', 't'], help='proxy workload: Gaussian or Student-t')
     ap.add_argument('--lv-mode', type=int, default=0, help='lv workload: 0 two-phase (default), 1 single-phase')
@@ -598,6 +689,11 @@ def main():
         hop = rank_hop(elapsed / args.steps * 1e3, integrand, m, rank, world, dev)
     if sharded and world > 1 and not args.no_config5 and args.config == 'c4':
         c5 = config5_sharded(rank, world, dev)
+    cog = chains_over_gpus(rank, 1, dev)
+    if sharded and world > 1 and not args.no_chains and args.config == 'c4':
+        _set_guard(None)   # the drop-in default (guard on unless ST_NEAR_TIE=0), as the reference's call gets it
+        cog = chains_over_gpus(rank, world, dev)
+        _set_guard(bool(args.headline_guard))
 
     roofline = None
     cpu = None
@@ -822,6 +918,7 @@ def main():
             'degraded': degraded,
             'rank_hop': hop,
             'config5_sharded': c5,
+            'chains_over_gpus': cog,
             'roofline': roofline,
             'cpu_baseline': cpu,
             'end_to_end': e2e if rank == 0 and not sharded else None,

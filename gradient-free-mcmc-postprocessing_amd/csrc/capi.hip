@@ -97,7 +97,7 @@ int st_tune(int32_t key, int32_t value) {
     else if (key == 17) rc = st::lv_tune(value);
     else if (key == 18) rc = st::lv_pieces_tune(value);
     else rc = ((key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12 || key == 15 || key == 16 ||
-               key == 19)
+               key == 19 || key == 23)
                   ? st::persistent_tune(key, value)
                   : st::tune(key, value);
     if (rc != 0) return fail(ST_ERR_INVALID, "bad tuning key/value %d=%d", key, value);
@@ -106,7 +106,7 @@ int st_tune(int32_t key, int32_t value) {
 
 int32_t st_tune_get(int32_t key) {
     const bool persist = (key >= 3 && key <= 5) || key == 8 || key == 9 || key == 10 || key == 12 || key == 15 ||
-                         key == 16 || key == 19;
+                         key == 16 || key == 19 || key == 23;
     return persist ? st::persistent_tune_get(key) : st::tune_get(key);
 }
 

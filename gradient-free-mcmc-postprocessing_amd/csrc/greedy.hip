@@ -436,11 +436,15 @@ static int g_max_blocks = 256;
 static int g_cpt = -1;
 static int g_pf = -1;
 static int g_rt_max_blocks = kMaxBlocks;
-static int g_arith = 1;   // st_tune key 11
+static int g_arith = 1;   // st_tune key 11 (process-wide)
+// st_tune key 22: the calling host thread's own arithmetic (-1: none, the process-wide key 11 applies) --
+// stein_thinning.arithmetic_override, so that threads thinning side by side (thin_chains: one per GPU)
+// never change each other's launches
+static thread_local int t_arith = -1;
 static int g_tie_guard = 1;   // st_tune key 20
 constexpr int64_t kLargeShard = 1000000;
 
-int arith_compact() { return g_arith; }
+int arith_compact() { return t_arith >= 0 ? t_arith : g_arith; }
 int tie_guard() { return g_tie_guard; }
 
 int tune_get(int key) {
@@ -451,6 +455,7 @@ int tune_get(int key) {
         case 6: return g_rt_max_blocks;
         case 11: return g_arith;
         case 20: return g_tie_guard;
+        case 22: return t_arith;
         default: return INT32_MIN;
     }
 }
@@ -459,6 +464,7 @@ int tune(int key, int value) {
     switch (key) {
         case 11: if (value < -1 || value > 1) return -1; g_arith = value < 0 ? 1 : value; return 0;
         case 20: if (value < -1 || value > 1) return -1; g_tie_guard = value < 0 ? 1 : value; return 0;
+        case 22: if (value < -1 || value > 1) return -1; t_arith = value; return 0;
         case 6: if (value < 1 || value > kMaxBlocks) return -1; g_rt_max_blocks = value; return 0;
         case 0: if (value < 1 || value > kMaxBlocks) return -1; g_max_blocks = value; return 0;
         case 1: if (value != -1 && value != 1 && value != 2 && value != 4) return -1; g_cpt = value; return 0;

@@ -44,6 +44,10 @@ int64_t persistent_ws_max_bytes() {
 static int g_persist_rt = -1;   // st_tune key 3: -1 auto, 0 = off
 static int g_persist_nt = -1;   // st_tune key 4: threads per block, -1 auto (256)
 static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (one per CU)
+// st_tune key 23: the calling host thread's own grid cap (-1: none; greedy_concurrent's streams), so that
+// threads thinning side by side never change each other's grids
+static thread_local int t_persist_grid = -1;
+static int grid_cap() { return t_persist_grid > 0 ? t_persist_grid : g_persist_grid; }
 static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
 static int g_persist_pitch = -1; // st_tune key 9: record pitch in bytes (16 .. 4096, power of 2), -1 auto
 static int g_persist_nrep = -1;  // st_tune key 10: record replicas (1 .. 32, power of 2), -1 auto
@@ -86,6 +90,7 @@ int persistent_tune_get(int key) {
         case 3: return g_persist_rt;
         case 4: return g_persist_nt;
         case 5: return g_persist_grid;
+        case 23: return t_persist_grid;
         case 8: return g_persist_bpc;
         case 9: return g_persist_pitch;
         case 10: return g_persist_nrep;
@@ -111,6 +116,11 @@ int persistent_tune(int key, int value) {
     if (key == 5) {
         if (value < -1 || value == 0 || value > kMaxGrid) return -1;
         g_persist_grid = value;
+        return 0;
+    }
+    if (key == 23) {
+        if (value < -1 || value == 0 || value > kMaxGrid) return -1;
+        t_persist_grid = value;
         return 0;
     }
     if (key == 8) {
@@ -345,9 +355,9 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     if (wide) rt = 1;
     const bool gf = w != nullptr;
     const size_t row_bytes = (size_t)(2 * d + 1 + (gf ? 1 : 0)) * sizeof(double);
-    // near-tie guard: one device, the compact arithmetic, d = 2 / 4 (st_tune key 20) -- the GUARD kernels,
-    // whose LDS holds the guard's scratch after Scratch
-    const bool guard = tie_guard() && arith_compact() && !wide && rs->nranks == 1 && !plan_only;
+    // near-tie guard: the compact arithmetic, d = 2 / 4 (st_tune key 20), one device or every rank of a
+    // multi-rank run -- the GUARD kernels, whose LDS holds the guard's scratch after Scratch
+    const bool guard = tie_guard() && arith_compact() && !wide && !plan_only;
     // (the 256-thread guarded kernels also hold every thread's step record, GuardLanes)
     const size_t head = (sizeof(Scratch) + 15) / 16 * 16 + (guard ? (sizeof(GuardScratch) + 15) / 16 * 16 : 0) +
                         (guard && nt != 512 ? (sizeof(GuardLanes) + 15) / 16 * 16 : 0);
@@ -432,6 +442,9 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
             // 5 x 512 rows, then 6 (profiles/r05_mid_rows_probe.log: 8 never won below 8 x 512)
             rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R <= 5 * 512 ? 4 : 6);
         while (cmp_force <= 0 && rt_c > 8 && (int64_t)rt_c * 512 > R) --rt_c;   // no empty register rows
+        // guarded: at most 8 register rows -- the guard's rescans take the registers a ninth row needs (9 / 10
+        // rows spill inside the step loop: +38 % at config 4 in round 5; 8 rows keep the sweep spill-free)
+        if (guard && rt_c > 8) rt_c = 8;
         int64_t RLc = 0;
         int salc = 0;
         lds_rows(512, rt_c, RLc, lds_c, salc);
@@ -471,6 +484,44 @@ static hipError_t prepare_ws(Plan& P, hipStream_t s) {
     return hipSuccess;
 }
 
+// The near-tie guard's bounds over ALL n rows (stein_ref.c sr_tie_bounds; the staging's operations): a
+// multi-rank run's blocks cover only their rank's rows, so the host merges every row's maxima into the
+// workspace words before the launch -- the blocks' own merges then change nothing, and every rank's
+// threshold recurrence is the single-device one
+template <int D, bool GF>
+__global__ __launch_bounds__(256) void tie_bounds_kernel(const double* g, const double* w, int64_t n, int64_t ld,
+                                                          double* bounds) {
+    double gm = 0.0, wm = GF ? 0.0 : 1.0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        double s2 = g[i] * g[i];
+#pragma unroll
+        for (int k = 1; k < D; ++k) s2 = s2 + g[k * ld + i] * g[k * ld + i];
+        gm = __builtin_fmax(gm, __builtin_isnan(s2) ? INFINITY : s2);
+        if constexpr (GF) wm = __builtin_fmax(wm, __builtin_isnan(w[i] * w[i]) ? INFINITY : w[i] * w[i]);
+    }
+    gm = wave_max_f64(gm);
+    wm = wave_max_f64(wm);
+    if ((threadIdx.x & 63) == 0) {
+        uint64_t* bw = reinterpret_cast<uint64_t*>(bounds);
+        __hip_atomic_fetch_max(bw, (uint64_t)__double_as_longlong(gm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_fetch_max(bw + 1, (uint64_t)__double_as_longlong(wm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+static hipError_t launch_tie_bounds(const PersistArgs& a, int d, hipStream_t s) {
+    const int64_t want = (a.n + 255) / 256;
+    const int blocks = (int)(want < 1024 ? want : 1024);
+    double* bounds = const_cast<double*>(a.tie_bounds);
+    if (d == 2) {
+        if (a.w) tie_bounds_kernel<2, true><<<blocks, 256, 0, s>>>(a.g, a.w, a.n, a.ld, bounds);
+        else tie_bounds_kernel<2, false><<<blocks, 256, 0, s>>>(a.g, a.w, a.n, a.ld, bounds);
+    } else {
+        if (a.w) tie_bounds_kernel<4, true><<<blocks, 256, 0, s>>>(a.g, a.w, a.n, a.ld, bounds);
+        else tie_bounds_kernel<4, false><<<blocks, 256, 0, s>>>(a.g, a.w, a.n, a.ld, bounds);
+    }
+    return hipGetLastError();
+}
+
 // Returns hipErrorNotSupported when the persistent path does not apply (caller falls back).
 hipError_t launch_greedy_persistent(const double* x, const double* g, const double* w, double* A,
                                     int64_t n, int d, int64_t ld, double l, double tr, int64_t m,
@@ -479,9 +530,10 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
     *used = 0;
     Plan P;
     hipError_t e = plan_persistent(x, g, w, A, n, d, ld, l, tr, m, idx_out, ws, ws_bytes, s, used, rs, plan_only,
-                                   g_persist_grid, P);
+                                   grid_cap(), P);
     if (e != hipSuccess || plan_only) return e;
     if ((e = prepare_ws(P, s)) != hipSuccess) return e;
+    if (P.a.tie_bounds && P.a.nranks > 1 && (e = launch_tie_bounds(P.a, P.d, s)) != hipSuccess) return e;
     if (P.use_cmp) {
         if ((e = launch_cmp(P.ac, P.d, P.gf, P.rt_c, P.G, P.lds_c, s, false)) != hipSuccess) return e;
         // the shared record region is zeroed again between the two launches (see above)
@@ -507,7 +559,7 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
         hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         return hipErrorNotSupported;
     int cap = cus / count;
-    if (g_persist_grid > 0 && cap > g_persist_grid) cap = g_persist_grid;
+    if (grid_cap() > 0 && cap > grid_cap()) cap = grid_cap();
     if (cap < 1) return hipErrorNotSupported;
     Plan P[kMaxBatch];
     BatchArgs bc{}, bg{};

@@ -21,10 +21,8 @@ const void* kernel(bool batch) {
 // the plans launch_p instantiates (persistent.hip launch_p_cmp / launch_p_rt), compact arithmetic
 template <int D, bool GF>
 const void* pick(int rt, int nt, int bpc, bool gen, bool batch) {
-    if (!gen) {   // compact-only kernels: 512 threads, 8 .. 10 register rows
-        if (nt != 512 || bpc != 1) return nullptr;
-        if (rt >= 10) return kernel<D, GF, 10, 512, 1, false>(batch);
-        if (rt == 9) return kernel<D, GF, 9, 512, 1, false>(batch);
+    if (!gen) {   // compact-only kernels: 512 threads, 8 register rows (guarded plans use no more: persistent.hip)
+        if (nt != 512 || bpc != 1 || rt != 8) return nullptr;
         return kernel<D, GF, 8, 512, 1, false>(batch);
     }
     if (bpc == 2) {

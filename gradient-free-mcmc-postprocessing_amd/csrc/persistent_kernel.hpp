@@ -54,38 +54,40 @@ __device__ __forceinline__ void p_wave_minloc(double& v, int64_t& i) { wave_minl
 struct Scratch {          // small per-block scratch at the start of the dynamic LDS region
     double row[2 * kWideD + 2];   // winner row {x[d], g[d], w}
     double vblk;          // this block's last published minimum (NaN iff some row's A is NaN)
-    uint64_t wk[kMaxPWaves]; // per-wave minima as value_key (publish), then
-    int64_t i[kMaxPWaves];   // their indices; i[0] also carries the step's winner to the block
+    uint64_t wk[kMaxPWaves]; // per-wave minima as value_key (publish) and
+    int64_t i[kMaxPWaves];   // their rows: valid until the next publish (the guard's rescans combine them)
+    int64_t win;          // the step's winner, from the picking wave to the block
     int abort;
     int rowfast;          // wide d: the winner row lies in the fast range (set by the fetching wave)
     int ctr[2];           // 512-thread blocks: per-step chunk counters (dynamic LDS / streamed rows)
 };
 
-// near-tie guard state (GUARD kernels only: after Scratch in the dynamic LDS), by step parity: the
-// rescan's per-wave minimum, its row and the wave's second-smallest sum; the step's winner (row and sum;
-// tie_check reads its score row and weight from the inputs) and this block's published minimum; the
-// threshold recurrence
+// near-tie guard state (GUARD kernels only: after Scratch in the dynamic LDS), by step parity: per wave,
+// the rescan's smallest sum of the block's rows other than the block's minimum row and its bitwise
+// duplicates ("other"); the step's winner (row and sum; tie_check reads its score row and weight from the
+// inputs) and this block's published minimum and its row; the threshold recurrence
 struct GuardScratch {
-    double rs_min[2][kMaxPWaves], rs_run[2][kMaxPWaves];
-    uint32_t rs_idx[2][kMaxPWaves];
-    uint32_t win_i[2];
+    double rs_o[2][kMaxPWaves];
+    uint32_t win_i[2], blk_i[2];
     double win_v[2], blk_v[2];
     double tg[6];         // recurrence state (stein_ref.c tie_state): c1, wmax, Dmax, Q, E, thr
     double bnd[kMaxPWaves][2];   // per wave: max_i |g_i|^2, max_i w_i^2 over its rows (staging)
     // 512-thread kernels: wave 0's per-lane rescan of its register rows (step t - 1, written at the start
-    // of step t), reduced by wave 1 after publishing step t, off the critical path
-    double w0_b[64], w0_b2[64];
-    uint32_t w0_bi[64];
+    // of step t) -- the lane's "other" and the mask of its register rows whose sum equals the block's
+    // minimum -- finished (duplicate test) and reduced by wave 1 after publishing step t, off the critical path
+    double w0_o[64];
+    uint32_t w0_m[64];
     int tied;             // a step was flagged (this block's word was written)
 };
 
-// 256-thread GUARD kernels (no dynamic chunks): every thread's (minimum, its row, second-smallest) of a
-// step, by parity, after GuardScratch in the dynamic LDS.  Only the winner's block needs its block's
-// second-smallest sum (tie_check), so only that block reduces these -- the other blocks run no wave
-// reduction for the guard at all
+// 256-thread GUARD kernels (no dynamic chunks): every thread's "other" of a step and the mask of its
+// register rows still to be tested for being duplicates of the block's minimum row (wave 0's threads; the
+// other waves test theirs while rescanning), by parity, after GuardScratch in the dynamic LDS.  Only the
+// winner's block, or a block whose minimum equals the winner's sum, needs its "other" (tie_check), so
+// only such a block reduces these -- the other blocks run no wave reduction for the guard at all
 struct GuardLanes {
-    double b[2][256], b2[2][256];
-    uint32_t bi[2][256];
+    double o[2][256];
+    uint32_t m[2][256];
 };
 
 // Per-thread argmin scan: every thread visits its rows in increasing index order, so a candidate
@@ -234,10 +236,11 @@ struct PersistArgs {
     uint64_t seq_base;            // exchange sequence number of step 0 (mailbox banks / tags)
     uint64_t* inbox;              // this rank's mailbox (nranks > 1)
     uint64_t* peer[kMaxRanks];    // every rank's mailbox as mapped in this process
-    // near-tie guard of the compact arithmetic (one device; the GUARD kernels; nullptr = off): the
-    // problem's [max_i |g_i|^2, max_i w_i^2] -- every block merges its rows' maxima during staging (u64
-    // atomic max on the bit patterns) -- and the word receiving the first flagged step as ~step through
-    // an atomic max (0: none); tie[3] = 1 marks a guarded run
+    // near-tie guard of the compact arithmetic (the GUARD kernels; nullptr = off): the problem's
+    // [max_i |g_i|^2, max_i w_i^2] -- every block merges its rows' maxima during staging (u64 atomic max on
+    // the bit patterns); a multi-rank run's host has merged all n rows' beforehand -- and the word
+    // receiving the first flagged step as ~step through an atomic max (0: none); tie[3] = 1 marks a
+    // guarded run
     const double* tie_bounds;
     unsigned* tie;
 };
@@ -346,7 +349,10 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
             combine_waves<NT>(sc, k, ib);
             const double vb = key_value(k);
             sc->vblk = vb;   // read by every thread after wait_and_pick's barrier
-            if constexpr (GUARD) gsc->blk_v[t & 1] = vb;   // this block's minimum of step t
+            if constexpr (GUARD) {   // this block's minimum of step t and its row
+                gsc->blk_v[t & 1] = vb;
+                gsc->blk_i[t & 1] = ib;
+            }
             uint64_t* gr = a.gran + (t & 1) * a.rep_stride + (int64_t)bid * a.rec_stride;
             const uint64_t tag = step_tag(t);
             __hip_atomic_store(gr + 0, tag | (k >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -363,7 +369,10 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
         if (threadIdx.x == 0) {
             const double vb = key_value(k);
             sc->vblk = vb;
-            if constexpr (GUARD) gsc->blk_v[t & 1] = vb;   // this block's minimum of step t
+            if constexpr (GUARD) {   // this block's minimum of step t and its row
+                gsc->blk_v[t & 1] = vb;
+                gsc->blk_i[t & 1] = ib;
+            }
         }
         if ((int)threadIdx.x < a.nrep) {
             const uint64_t tag = step_tag(t);
@@ -396,37 +405,58 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 
 
 
-// ---- near-tie guard (compact arithmetic, one device) ------------------------------------------
-// Step t is flagged when the smallest running sum of any row other than the winner -- an exact tie
-// included -- lies within thr(t) of the winner's (oracle/stein_ref.c sr_greedy_mt_ties is the model: the
-// rule, the bound thr(t) and its recurrence).  Nothing is added to the pair loop or to the exchange's
-// critical path: after publishing step t the waves that do not sweep rescan the block's running sums
-// (already on chip: registers, LDS, and the streamed rows' sums in L2) for the minimum, its row and the
-// second-smallest sum per wave; the picking wave (wave 0) rescans its own register rows while its first
-// poll is in flight (512-thread kernels: right after the pick) and leaves one (minimum, row,
-// second-smallest) per lane in LDS, which wave 1 reduces after the next publish.  One step later
-// (during step t + 1's exchange) one lane checks step t: in the
-// winner's block, the block's second-smallest sum against the winner's; in every other block, the
-// block's minimum against it -- together exactly the model's rule -- and a flagged block writes ~t into
-// the tie word with an atomic max (the largest ~t = the first flagged step).  The same lane advances
-// the threshold recurrence.
-struct Top2 {   // a thread's rows: minimum (lowest row on ties) and second-smallest sum (ties count)
-    double b = INFINITY, b2 = INFINITY;
-    uint32_t bi = 0xFFFFFFFFu;
-    __device__ __forceinline__ void add(double a, uint32_t ia) {
-        const bool take = (a < b) | ((a == b) & (ia < bi));
-        b2 = __builtin_fmin(b2, take ? b : a);
-        b = take ? a : b;
-        bi = take ? ia : bi;
-    }
-    // another set's (minimum, row, second-smallest): the union's
-    __device__ __forceinline__ void merge(double a, double a2, uint32_t ia) {
-        const bool take = (a < b) | ((a == b) & (ia < bi));
-        b2 = __builtin_fmin(__builtin_fmin(b2, a2), take ? b : a);
-        b = take ? a : b;
-        bi = take ? ia : bi;
+// ---- near-tie guard (compact arithmetic) ------------------------------------------------------
+// Step t is flagged when the smallest running sum of any row other than the winner and its bitwise
+// duplicates -- any other exact tie included -- lies within thr(t) of the winner's (oracle/stein_ref.c
+// sr_greedy_mt_ties is the model: the rule, the bound thr(t) and its recurrence).  A row equal to the
+// winner bit for bit (x, g, w: a repeated MCMC row, adjacent or not) has the winner's sum at every step in
+// every arithmetic and loses the tie to the lower index on both paths, so it does not count.
+// Nothing is added to the pair loop or to the exchange's critical path.  After publishing step t the waves
+// that do not sweep rescan the block's running sums (already on chip: registers, LDS, and the streamed
+// rows' sums in L2) against the block's minimum vmin and its row ibk, both known from the publish: per
+// thread the smallest sum != vmin ("other"), and for the rows whose sum == vmin (other than ibk) a bitwise
+// comparison with row ibk -- a row that differs is a genuine tie and contributes vmin.  So "other" is the
+// smallest sum of the block's rows other than ibk and its duplicates.  The picking wave (wave 0) only
+// records its register rows' "other" and the mask of those tied with vmin (while its first poll is in
+// flight; 512-thread kernels: right after the pick); the comparison of those rows is done later by the
+// wave that reduces them (global loads of both rows), off the critical path.  One step later (during step
+// t + 1's exchange) one lane checks step t: in the winner's block (ibk = the winner), the block's "other";
+// in a block whose minimum equals the winner's sum exactly, its "other" if its row ibk duplicates the
+// winner, else that minimum; in every other block, its minimum -- together exactly the model's rule.  A
+// flagged block writes ~t into the tie word with an atomic max (the largest ~t = the first flagged step);
+// the same lane advances the threshold recurrence.  Multi-rank runs (nranks > 1): every rank's blocks run
+// the same check against the global winner (each rank flags its own rows; the host combines the ranks'
+// words with one all-reduce after the run) over bounds the host computed from all n rows beforehand.
+
+// the row (x, g[, w]) of row r from the read-only inputs
+template <int D, bool GF>
+struct RowBits {
+    double v[2 * D + (GF ? 1 : 0)];
+    __device__ __forceinline__ void load(const PersistArgs& a, int64_t r) {
+#pragma unroll
+        for (int k = 0; k < D; ++k) {
+            v[k] = a.x[(int64_t)k * a.ld + r];
+            v[D + k] = a.g[(int64_t)k * a.ld + r];
+        }
+        if constexpr (GF) v[2 * D] = a.w[r];
     }
 };
+
+__device__ __forceinline__ bool same_bits(double p, double q) {
+    return __double_as_longlong(p) == __double_as_longlong(q);
+}
+
+template <int D, bool GF>
+__device__ __forceinline__ bool rows_equal(const RowBits<D, GF>& p, const RowBits<D, GF>& q) {
+    bool eq = true;
+#pragma unroll
+    for (int k = 0; k < 2 * D + (GF ? 1 : 0); ++k) eq &= same_bits(p.v[k], q.v[k]);
+    return eq;
+}
+
+// a sum's contribution to "other": everything but the block's minimum value (rows tied with it are
+// tested separately)
+__device__ __forceinline__ double other_of(double a, double vmin) { return a == vmin ? INFINITY : a; }
 
 __device__ __forceinline__ double wave_max_f64(double m) {
     m = __builtin_fmax(m, dpp_f64<0xB1>(m));
@@ -454,23 +484,26 @@ __device__ __forceinline__ double wave_min_f64(double m) {
     return __builtin_fmin(__builtin_fmin(r0, r1), __builtin_fmin(r2, r3));
 }
 
-// the calling wave's (minimum, its row, second-smallest) into slot [par][wave]; every lane active
-__device__ __forceinline__ void top2_wave(GuardScratch* sc, const Top2& r, int par, int w = -1) {
-    double v = r.b;
-    int64_t i = r.bi == 0xFFFFFFFFu ? INT64_MAX : (int64_t)r.bi;
-    p_wave_minloc(v, i);
-    const double c = wave_min_f64((r.bi != 0xFFFFFFFFu && (int64_t)r.bi == i) ? r.b2 : r.b);
-    if ((threadIdx.x & 63) == 0) {
-        if (w < 0) w = threadIdx.x >> 6;
-        sc->rs_min[par][w] = v;
-        sc->rs_idx[par][w] = i == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)i;
-        sc->rs_run[par][w] = c;
+// The duplicate test of register rows recorded as a mask (wave 0's rows): thread `owner`'s register rows
+// q set in `msk` (rows r0 + q * NT + owner, sum == vmin) are compared with row ibk through global loads; a
+// row that differs contributes vmin.  Per lane; the caller keeps it behind a wave-uniform branch.
+template <int D, bool GF, int NT>
+__device__ __forceinline__ double finish_mask(const PersistArgs& a, double o, uint32_t msk, int owner, int64_t r0,
+                                              double vmin, const RowBits<D, GF>& b) {
+    while (msk) {
+        const int q = __builtin_ctz(msk);
+        msk &= msk - 1;
+        RowBits<D, GF> r;
+        r.load(a, r0 + (int64_t)q * NT + owner);
+        if (!rows_equal(r, b)) o = __builtin_fmin(o, vmin);
     }
+    return o;
 }
 
 // one lane: the check of step t (its rescan and winner are in slot t & 1), then thr(t) -> thr(t + 1)
 // (stein_ref.c tie_init / tie_step, the same operations).  Step 0 first reads the problem's bounds,
-// which every block merged before publishing step 0 (so this block's sweep of step 0 saw them all)
+// which every block merged before publishing step 0 (so this block's sweep of step 0 saw them all), or
+// the host wrote before the launch (multi-rank: all n rows)
 template <int D, bool GF>
 __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc, int64_t t, int64_t r0, int64_t r1,
                                           int nwaves) {
@@ -493,13 +526,20 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
     }
     const double v = sc->win_v[par];
     const uint32_t gi = sc->win_i[par];
-    double other;
-    if ((int64_t)gi >= r0 && (int64_t)gi < r1) {   // the winner's block: its second-smallest sum
+    // a completed pick's row is always < n; so is a block's minimum row unless the block holds no row
+    const int64_t gr = (int64_t)gi < a.n ? (int64_t)gi : 0;
+    double other = sc->blk_v[par];
+    bool rest = (int64_t)gi >= r0 && (int64_t)gi < r1;   // the winner's block: its "other"
+    if (!rest && other == v) {   // this block's minimum ties the winner's sum: a duplicate of the winner?
+        const uint32_t bi = sc->blk_i[par];
+        RowBits<D, GF> p, q;
+        p.load(a, gr);
+        q.load(a, (int64_t)bi < a.n ? (int64_t)bi : 0);
+        rest = rows_equal(p, q);
+    }
+    if (rest) {
         other = INFINITY;
-        for (int w = 0; w < nwaves; ++w)
-            other = __builtin_fmin(other, sc->rs_idx[par][w] == gi ? sc->rs_run[par][w] : sc->rs_min[par][w]);
-    } else {
-        other = sc->blk_v[par];
+        for (int w = 0; w < nwaves; ++w) other = __builtin_fmin(other, sc->rs_o[par][w]);
     }
     if (other - v <= ts[5] && !sc->tied) {
         sc->tied = 1;
@@ -508,7 +548,6 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
     const double Q = ts[3] + v;
     // the winner's g (and w) from the read-only inputs: Scratch::row may already hold the next step's
     // winner (this check runs one step late, off the critical path, and the next pick does not wait)
-    const int64_t gr = (int64_t)gi < a.n ? (int64_t)gi : 0;   // a completed pick's row is always < n
     double gj[D];
 #pragma unroll
     for (int k = 0; k < D; ++k) gj[k] = a.g[(int64_t)k * a.ld + gr];
@@ -523,20 +562,35 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
     ts[5] = 0x1p-50 * (8.0 * ts[2] + E);
 }
 
-// tie_check for the 256-thread GUARD kernels (one whole wave): in the winner's block the wave reduces
-// the block's per-thread (minimum, row, second-smallest) of step t (GuardLanes) into rs slot 0, the
-// other blocks only compare their published minimum; then lane 0 runs tie_check on that one slot
+// tie_check for the 256-thread GUARD kernels (one whole wave): in a block that needs its "other" (the
+// winner's block, or one whose minimum equals the winner's sum) the wave finishes the duplicate test of
+// wave 0's recorded rows and reduces the block's per-thread "other" of step t (GuardLanes) into rs slot 0;
+// the other blocks only compare their published minimum; then lane 0 runs tie_check on that one slot
 template <int D, bool GF, int NT>
 __device__ __forceinline__ void tie_check_lanes(const PersistArgs& a, GuardScratch* sc, const GuardLanes* gl,
                                                 int64_t t, int64_t r0, int64_t r1) {
     static_assert(NT <= 256, "GuardLanes holds 256 threads");
     const int par = (int)(t & 1);
     const uint32_t gi = sc->win_i[par];
-    if ((int64_t)gi >= r0 && (int64_t)gi < r1) {   // block-uniform
-        Top2 r;
+    const double vmin = sc->blk_v[par];
+    if (((int64_t)gi >= r0 && (int64_t)gi < r1) || vmin == sc->win_v[par]) {   // block-uniform
+        const int lane = (int)(threadIdx.x & 63);
+        double o = INFINITY;
+        uint32_t any = 0;
 #pragma unroll
-        for (int k = (int)(threadIdx.x & 63); k < NT; k += 64) r.merge(gl->b[par][k], gl->b2[par][k], gl->bi[par][k]);
-        top2_wave(sc, r, par, 0);
+        for (int k = lane; k < NT; k += 64) {
+            o = __builtin_fmin(o, gl->o[par][k]);
+            any |= gl->m[par][k];
+        }
+        if (__any(any != 0)) {
+            const uint32_t bi = sc->blk_i[par];
+            RowBits<D, GF> b;
+            b.load(a, (int64_t)bi < a.n ? (int64_t)bi : 0);
+#pragma unroll
+            for (int k = lane; k < NT; k += 64) o = finish_mask<D, GF, NT>(a, o, gl->m[par][k], k, r0, vmin, b);
+        }
+        o = wave_min_f64(o);
+        if (lane == 0) sc->rs_o[par][0] = o;
     }
     if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, t, r0, r1, 1);
 }
@@ -840,7 +894,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
             // (max: a compact-only kernel's "needs the exact arithmetic" (2) is not overwritten)
             if (!ok_all) __hip_atomic_fetch_max(a.status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             sc->abort = !ok_all;
-            sc->i[0] = gi;
+            sc->win = gi;
             if constexpr (GUARD) {
                 if (guard) {
                     gsc->win_i[t & 1] = gi == INT64_MAX ? 0xFFFFFFFFu : (uint32_t)gi;
@@ -852,7 +906,7 @@ __device__ __forceinline__ int64_t wait_and_pick(const PersistArgs& a, Scratch* 
     __syncthreads();
     ST_STAMP(a, t + 1, 2);
     if (sc->abort) return -1;
-    return sc->i[0];
+    return sc->win;
 }
 
 // BPC = blocks per CU: 2 puts two 256-thread blocks on each CU (two waves per SIMD, RT <= 8
@@ -1103,57 +1157,127 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     publish<NT, GUARD>(a, sc, bv, bi, 0, r1, bid(), gsc);
 
     // near-tie guard: the rescans of the block's running sums after each publish (module comment above
-    // tie_check).  Wave 0: its register rows (inside wait_and_pick, while its first poll is in flight);
-    // the other waves: their register rows and, dealt statically over their threads, the LDS and
-    // streamed rows.
+    // tie_check).  Wave 0: its register rows (inside wait_and_pick, while its first poll is in flight; the
+    // 512-thread kernels at the start of the next step), the duplicate test of its tied rows left to the
+    // wave that reduces them; the other waves: their register rows and, dealt statically over their
+    // threads, the LDS and streamed rows, duplicate test included.
     constexpr int kNW = NT / 64;
-    auto rescan_regs = [&](Top2& r) {
+    // register rows: "other" and the mask of the rows whose sum equals vmin (other than ibk).  No row test:
+    // padding rows hold +inf, which changes neither (a tie at +inf would contribute +inf: ignored)
+    auto rescan_regs = [&](double vmin, uint32_t ibk, double& o, uint32_t& msk) {
+        const uint32_t row0 = (uint32_t)(r0 + tid);
+        const bool fin = vmin < INFINITY;
 #pragma unroll
         for (int q = 0; q < RT; ++q) {
-            const int64_t row = r0 + (int64_t)q * kPBlock + tid;
-            if (row < r1) r.add(ar[q], (uint32_t)row);
+            o = __builtin_fmin(o, other_of(ar[q], vmin));
+            msk |= ((ar[q] == vmin) & fin & (row0 + (uint32_t)(q * kPBlock) != ibk)) ? 1u << q : 0u;
         }
     };
-    auto rescan_rest = [&](int64_t tt) {   // waves 1 .. kNW - 1
-        Top2 r;
-        rescan_regs(r);
+    auto rescan_rest = [&](int64_t tt) {   // waves 1 .. kNW - 1, right after publish(tt)
+        // the block's minimum and its row, combined from the wave minima publish(tt) left in Scratch (wave 0
+        // writes blk_v / blk_i only after publish's barrier)
+        uint64_t kmin;
+        uint32_t ibk;
+        combine_waves<NT>(sc, kmin, ibk);
+        const double vmin = key_value(kmin);
+        double o = INFINITY;
+        uint32_t msk = 0;
+        bool tie = false;   // an LDS or streamed row tied with vmin
+        rescan_regs(vmin, ibk, o, msk);
         if constexpr (!kWide) {
-            for (int e = tid - 64; e < RL; e += kPBlock - 64)
-                if (lds_base + e < r1) r.add(lrow(e)[fA], (uint32_t)(lds_base + e));
-            for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64)
-                r.add((kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row], (uint32_t)row);
+            for (int e = tid - 64; e < RL; e += kPBlock - 64) {
+                const int64_t row = lds_base + e;
+                const double av = lrow(e)[fA];
+                if (row < r1) {
+                    o = __builtin_fmin(o, other_of(av, vmin));
+                    tie |= av == vmin && (uint32_t)row != ibk;
+                }
+            }
+            for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64) {
+                const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
+                o = __builtin_fmin(o, other_of(av, vmin));
+                tie |= av == vmin && (uint32_t)row != ibk;
+            }
         }
-        if constexpr (kLanes) {   // per thread, reduced only in the winner's block (tie_check_lanes)
-            const int par = (int)(tt & 1);
-            gl->b[par][tid] = r.b;
-            gl->b2[par][tid] = r.b2;
-            gl->bi[par][tid] = r.bi;
+        if (__any(msk != 0 || tie)) {   // rows tied with the block's minimum: duplicates of row ibk?
+            RowBits<D, GF> b;
+            b.load(a, (int64_t)ibk < a.n ? (int64_t)ibk : 0);
+#pragma unroll
+            for (int q = 0; q < RT; ++q) {
+                if ((msk >> q) & 1u) {
+                    bool same = true;
+#pragma unroll
+                    for (int k = 0; k < D; ++k) {
+                        same &= same_bits(xr[q][k], b.v[k]);
+                        same &= same_bits(gr[q][k], b.v[D + k]);
+                    }
+                    if constexpr (GF) same &= same_bits(wr[q], b.v[2 * D]);
+                    if (!same) o = __builtin_fmin(o, vmin);
+                }
+            }
+            if constexpr (!kWide) {
+                for (int e = tid - 64; e < RL; e += kPBlock - 64) {
+                    const int64_t row = lds_base + e;
+                    const double* rp = lrow(e);
+                    if (row < r1 && rp[fA] == vmin && (uint32_t)row != ibk) {
+                        bool same = true;
+#pragma unroll
+                        for (int k = 0; k < D; ++k) {
+                            same &= same_bits(rp[fX + k * 64], b.v[k]);
+                            same &= same_bits(rp[fG + k * 64], b.v[D + k]);
+                        }
+                        if constexpr (GF) same &= same_bits(rp[fW], b.v[2 * D]);
+                        if (!same) o = __builtin_fmin(o, vmin);
+                    }
+                }
+                for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64) {
+                    const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
+                    if (av == vmin && (uint32_t)row != ibk) {
+                        RowBits<D, GF> r;
+                        r.load(a, row);
+                        if (!rows_equal(r, b)) o = __builtin_fmin(o, vmin);
+                    }
+                }
+            }
+        }
+        const int par = (int)(tt & 1);
+        if constexpr (kLanes) {   // per thread, reduced only where tie_check needs it (tie_check_lanes)
+            gl->o[par][tid] = o;
+            gl->m[par][tid] = 0u;
         } else {
-            top2_wave(gsc, r, (int)(tt & 1));
+            o = wave_min_f64(o);
+            if ((tid & 63) == 0) gsc->rs_o[par][wid] = o;
         }
     };
-    // wave 0's own rescan leaves one Top2 per lane in LDS; wave 1 reduces them after the next publish
-    int64_t t = 1;   // the step loop's counter (rescan_w0 of the 256-thread kernels files by its parity)
-    auto rescan_w0 = [&]() {
-        Top2 r;
-        rescan_regs(r);
-        if constexpr (kLanes) {   // inside wait_and_pick(t - 1): the sums of step t - 1
-            const int par = (int)((t - 1) & 1);
-            gl->b[par][tid] = r.b;
-            gl->b2[par][tid] = r.b2;
-            gl->bi[par][tid] = r.bi;
+    // wave 0's own rescan leaves its lanes' "other" and tied-row masks in LDS; the duplicate test and the
+    // reduction follow after the next publish (wave 1: reduce_w0; the 256-thread kernels: tie_check_lanes)
+    int64_t t = 1;   // the step loop's counter (rescan_w0 files by the parity of step t - 1)
+    auto rescan_w0 = [&]() {   // the sums of step t - 1; blk_v / blk_i were written by this wave's lane 0
+        const int par = (int)((t - 1) & 1);
+        double o = INFINITY;
+        uint32_t msk = 0;
+        rescan_regs(gsc->blk_v[par], gsc->blk_i[par], o, msk);
+        if constexpr (kLanes) {   // inside wait_and_pick(t - 1)
+            gl->o[par][tid] = o;
+            gl->m[par][tid] = msk;
         } else {
-            gsc->w0_b[tid] = r.b;
-            gsc->w0_b2[tid] = r.b2;
-            gsc->w0_bi[tid] = r.bi;
+            gsc->w0_o[tid] = o;
+            gsc->w0_m[tid] = msk;
         }
     };
-    auto reduce_w0 = [&](int64_t tt) {   // wave 1
-        Top2 r;
-        r.b = gsc->w0_b[tid - 64];
-        r.b2 = gsc->w0_b2[tid - 64];
-        r.bi = gsc->w0_bi[tid - 64];
-        top2_wave(gsc, r, (int)(tt & 1), 0);
+    auto reduce_w0 = [&](int64_t tt) {   // wave 1: wave 0's lanes of step tt
+        const int par = (int)(tt & 1);
+        const int lane = tid - 64;
+        double o = gsc->w0_o[lane];
+        const uint32_t msk = gsc->w0_m[lane];
+        if (__any(msk != 0)) {
+            const uint32_t ibk = gsc->blk_i[par];
+            RowBits<D, GF> b;
+            b.load(a, (int64_t)ibk < a.n ? (int64_t)ibk : 0);
+            o = finish_mask<D, GF, NT>(a, o, msk, lane, r0, gsc->blk_v[par], b);
+        }
+        o = wave_min_f64(o);
+        if (lane == 0) gsc->rs_o[par][0] = o;
     };
     if constexpr (guard) {
         if (wid >= 1) rescan_rest(0);

@@ -166,10 +166,15 @@ ARITHMETIC = {'exact': 0, 'compact': 1}
 _ARITH = 'compact'   # what the loaded library was last told (its default until then)
 
 
+_TL = threading.local()   # this host thread's arithmetic_override (st_tune key 22), None: the process mode
+
+
 def arithmetic() -> str:
-    """The arithmetic the greedy kernels use now ('compact' or 'exact'; set_arithmetic / ST_ARITH)."""
+    """The arithmetic the greedy kernels launched from this thread use now ('compact' or 'exact'):
+    an enclosing arithmetic_override, else the process-wide mode (set_arithmetic / ST_ARITH)."""
     lib()
-    return _ARITH
+    mode = getattr(_TL, 'mode', None)
+    return _ARITH if mode is None else mode
 
 
 def set_arithmetic(mode: str) -> None:
@@ -208,8 +213,10 @@ def near_tie_guard() -> bool:
 
 
 class arithmetic_override:
-    """``with arithmetic_override('exact'): ...`` -- the greedy kernels' arithmetic for the launches
-    enqueued inside the block (st_tune key 11 is process-wide; the previous mode is restored)."""
+    """``with arithmetic_override('exact'): ...`` -- the greedy kernels' arithmetic for the launches this
+    host thread enqueues inside the block.  Thread-local (st_tune key 22: the library keeps the override
+    per host thread), so concurrent threads -- thin_chains runs one per GPU -- never see each other's
+    mode; blocks nest (the previous override is restored on exit)."""
 
     def __init__(self, mode: str):
         if mode not in ARITHMETIC:
@@ -217,14 +224,34 @@ class arithmetic_override:
         self.mode = mode
 
     def __enter__(self):
-        self.prev = arithmetic()
-        if self.mode != self.prev:
-            set_arithmetic(self.mode)
+        L = lib()
+        self.prev = getattr(_TL, 'mode', None)
+        check(L.st_tune(22, ARITHMETIC[self.mode]), 'arithmetic_override')
+        _TL.mode = self.mode
         return self
 
     def __exit__(self, *exc):
-        if self.mode != self.prev:
-            set_arithmetic(self.prev)
+        check(lib().st_tune(22, -1 if self.prev is None else ARITHMETIC[self.prev]), 'arithmetic_override')
+        _TL.mode = self.prev
+        return False
+
+
+class grid_cap:
+    """``with grid_cap(k): ...`` -- at most k blocks per persistent-kernel grid for the launches this host
+    thread enqueues inside the block (st_tune key 23, per host thread; st_tune key 5 is the process-wide
+    cap); k <= 0: no cap of this thread's own."""
+
+    def __init__(self, blocks: int):
+        self.blocks = int(blocks)
+
+    def __enter__(self):
+        L = lib()
+        self.prev = int(L.st_tune_get(23))
+        check(L.st_tune(23, self.blocks if self.blocks > 0 else -1), 'grid_cap')
+        return self
+
+    def __exit__(self, *exc):
+        check(lib().st_tune(23, self.prev), 'grid_cap')
         return False
 
 
@@ -252,15 +279,24 @@ def check(rc: int, what: str = '') -> None:
         raise HipExtensionError(f'{what}: HIP error ({rc}): {msg}')
 
 
+# worker processes of the pools the reference fans thin() out with (joblib's loky / multiprocessing backends,
+# concurrent.futures): "LokyProcess-3", "ForkPoolWorker-3", "SpawnPoolWorker-3", "ForkServerPoolWorker-3",
+# "SpawnProcess-3" / "ForkProcess-3" / "ForkServerProcess-3" (ProcessPoolExecutor).  A user's own
+# multiprocessing.Process ("Process-3") or a DataLoader worker is not a pool worker: no policy there.
+POOL_WORKER_NAMES = r'^(?:LokyProcess|ForkPoolWorker|SpawnPoolWorker|ForkServerPoolWorker|SpawnProcess|ForkProcess|' \
+                    r'ForkServerProcess)-(\d+)$'
+
+
 def select_device_index(count: int, env=None, worker: bool = False, pid: int = 0, worker_name: str = ''):
     """The device policy of a process (pure: tests call it with a mocked device count):
     * ``ST_DEVICE`` in the environment: that device (an index < count);
     * else ``LOCAL_RANK`` (torchrun / torch.distributed.run: one process per GPU): LOCAL_RANK % count;
-    * else, in a worker process of a pool (joblib / loky / multiprocessing / Dask -- the reference fans
-      ``thin`` out over chains in such workers, ``code/src/utils/parallel.py:48-52``) with several
-      devices: the worker's ordinal from its process name ("LokyProcess-3", "ForkPoolWorker-3",
-      "SpawnProcess-3": (3 - 1) % count -- the pool's workers round-robin over the GPUs), or its
-      pid % count when the name carries none;
+    * else, in a worker process of a pool (joblib's loky / multiprocessing backends, concurrent.futures --
+      the reference fans ``thin`` out over chains in such workers, ``code/src/utils/parallel.py:48-52``;
+      POOL_WORKER_NAMES) with several devices: the worker's ordinal from its process name
+      ("LokyProcess-3", "ForkPoolWorker-3", "SpawnProcess-3": (3 - 1) % count -- the pool's workers
+      round-robin over the GPUs), a Dask nanny worker ("Dask Worker process ...") its pid % count; any other
+      child process (a user's own multiprocessing.Process, a DataLoader worker) gets no policy;
     * else None: the current torch device (cuda:0 unless the caller chose another).
     Returns the device index or None."""
     env = os.environ if env is None else env
@@ -278,8 +314,11 @@ def select_device_index(count: int, env=None, worker: bool = False, pid: int = 0
         return int(v) % count
     if worker and count > 1:
         import re
-        k = re.search(r'-(\d+)$', worker_name or '')
-        return (int(k.group(1)) - 1) % count if k else pid % count
+        k = re.match(POOL_WORKER_NAMES, worker_name or '')
+        if k:
+            return (int(k.group(1)) - 1) % count
+        if (worker_name or '').startswith('Dask Worker'):   # Dask's nanny workers carry no ordinal: the pid
+            return pid % count
     return None
 
 
@@ -304,19 +343,25 @@ def require_device():
     global _DEVICE_POLICY_DONE
     if not _DEVICE_POLICY_DONE:
         _DEVICE_POLICY_DONE = True
-        import multiprocessing
-        idx = select_device_index(torch.cuda.device_count(), os.environ, _pool_worker(), os.getpid(),
-                                  multiprocessing.current_process().name)
-        if idx is not None and idx != torch.cuda.current_device():
+        idx = _policy_index()
+        # a device the caller already chose (torch.cuda.set_device / with torch.cuda.device(k): not the
+        # default 0) is kept; the policy only moves a process that is still on the default device
+        if idx is not None and idx != torch.cuda.current_device() and torch.cuda.current_device() == 0:
             torch.cuda.set_device(idx)
     return torch.device('cuda', torch.cuda.current_device())
+
+
+def _policy_index():
+    import multiprocessing
+    import torch
+    return select_device_index(torch.cuda.device_count(), os.environ, _pool_worker(), os.getpid(),
+                               multiprocessing.current_process().name)
 
 
 def policy_pinned() -> bool:
     """True when the process's device comes from the policy (ST_DEVICE, LOCAL_RANK, a pool worker):
     thin_chains then keeps every chain on that device instead of spreading them over all GPUs."""
-    import torch
-    return select_device_index(torch.cuda.device_count(), os.environ, _pool_worker(), os.getpid()) is not None
+    return _policy_index() is not None
 
 
 def stream_handle():

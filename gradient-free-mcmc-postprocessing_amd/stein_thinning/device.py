@@ -241,9 +241,9 @@ class DeviceProblem:
         ``margins=True``: (indices, diagnostics.GreedyMargins) -- the same selection with each step's
         argmin margin against the arithmetic's error band (launch-per-step kernels, one step at a time).
         ``dedup=True``: thin the run starts only (``dedup_view``) when repeated rows make that
-        worthwhile (``dedup_pays``) -- or, under the near-tie guard ('kernel' mode), whenever any row
-        repeats its predecessor, since the guard counts exact ties; ``dedup='always'``: whenever
-        dedup_view has a view.  Either way the same indices and running sums bit for bit.
+        worthwhile (``dedup_pays``); ``dedup='always'``: whenever dedup_view has a view.  Either way the
+        same indices and running sums bit for bit.  (The near-tie guard does not count a tie between rows
+        equal bit for bit, so repeated rows -- adjacent or not -- never flag a step.)
         ``guard=True`` (the drop-in thin): the near-tie guard (``guard_mode``); the indices are then the
         reference NumPy path's even where the compact arithmetic alone would select another row, and
         the sums those of whichever arithmetic ran.  ``self.near_tie``: the guard's verdict -- None (no
@@ -255,9 +255,7 @@ class DeviceProblem:
             return gm.indices, gm
         mode = self.guard_mode(guard)
         view = None
-        if mode == 'kernel' and dedup:
-            view = self.dedup_view(any_repeat=True)
-        elif dedup == 'always' or (dedup and self.dedup_pays(n_points)):
+        if dedup == 'always' or (dedup and self.dedup_pays(n_points)):
             view = self.dedup_view()
             if view is not None and dedup != 'always' and not self.dedup_pays(n_points, view.n_unique):
                 view = None
@@ -414,8 +412,6 @@ class DeviceProblem:
         return out.cpu().numpy()
 
 
-_GRID_CAP_LOCK = __import__('threading').Lock()
-
 # thins in flight at once in greedy_concurrent: 8 chains of the reference's LV call shape (5e5 rows,
 # m = 10 000, repeated rows dropped, run detection included) took 83 ms with 4 in flight (64-block
 # grids) and 156 ms with 2, against 258-264 ms one after the other (profiles/r04_chains_probe.log)
@@ -470,26 +466,20 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
     L = nat.lib()
     k = len(problems)
     c = max(1, min(k, in_flight if in_flight is not None else IN_FLIGHT))
-    if c == 1:   # one at a time, full grid
-        return [p.greedy(n_points, dedup=dedup) for p in problems]
+    if c == 1:   # one at a time, full grid (the guard as the plain thin has it: ADVICE r05)
+        return [p.greedy(n_points, dedup=dedup, guard=guard) for p in problems]
     cus = torch.cuda.get_device_properties(problems[0].device).multi_processor_count
     views, modes = [], []
     for p in problems:
         v = None
         mode = p.guard_mode(guard)
-        if mode == 'kernel' and dedup:
-            v = p.dedup_view(any_repeat=True)
-        elif dedup == 'always' or (dedup and p.dedup_pays(n_points)):
+        if dedup == 'always' or (dedup and p.dedup_pays(n_points)):
             v = p.dedup_view()
             if v is not None and dedup != 'always' and not p.dedup_pays(n_points, v.n_unique):
                 v = None
         views.append(v)
         modes.append(mode)
     runs = [v.problem if v is not None else p for p, v in zip(problems, views)]
-    for i, (p, mode) in enumerate(zip(runs, modes)):   # no near-tie flag on their kernels: exact, one by one
-        if mode == 'exact':
-            bufs_exact = p._greedy_run(n_points, 'exact')[0]
-            modes[i] = ('done', bufs_exact)
     cur = torch.cuda.current_stream()
     bufs, streams = [None] * k, [None] * k
     kb = max(1, min(8, batch if batch is not None else BATCH))
@@ -504,14 +494,15 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
             by_n = sorted(part, key=lambda i: runs[i].n)
             try_batch(by_n[:len(by_n) // 2])
             try_batch(by_n[len(by_n) // 2:])
-    if kb > 1:   # batch launches over groups of one d (and weights or none), in order
-        groups = {}
+    if kb > 1:   # batch launches over groups of one d (and weights or none), in order; the batch kernel
+        groups = {}   # runs the compact arithmetic, so the problems the guard runs exactly go to the streams
         for i, p in enumerate(runs):
-            groups.setdefault((p.d, p.w is not None), []).append(i)
+            if modes[i] != 'exact':
+                groups.setdefault((p.d, p.w is not None), []).append(i)
         for ids in groups.values():
             for j in range(0, len(ids), kb):
                 try_batch(ids[j:j + kb])
-    rest = [i for i in range(k) if bufs[i] is None and not isinstance(modes[i], tuple)]
+    rest = [i for i in range(k) if bufs[i] is None]
     c = max(1, min(len(rest), c))
     # c streams, problem i on stream i % c: at most c grids of #CU / c blocks are ever resident
     # together, so every grid fits beside the others
@@ -519,36 +510,30 @@ def greedy_concurrent(problems, n_points: int, in_flight: Optional[int] = None, 
     for s in pool:
         s.wait_stream(cur)   # the problems' arrays were written on the current stream
     if rest:
-        # the grid cap (st_tune key 5) is process-wide: set under a lock, the caller's value restored
-        with _GRID_CAP_LOCK:
-            prev = int(L.st_tune_get(5))
-            nat.check(L.st_tune(5, max(1, cus // c) if c > 1 else -1), 'st_tune')
-            try:
-                for j, i in enumerate(rest):
-                    s = pool[j % c]
-                    with torch.cuda.stream(s):
-                        b = runs[i].greedy_buffers(n_points)
-                        runs[i].greedy_launch(n_points, *b)
-                    bufs[i], streams[i] = b, s
-            finally:
-                L.st_tune(5, prev)
+        # this thread's grid cap (st_tune key 23) and, for the problems the guard runs exactly (d outside
+        # {2, 4}: kernels without a flag), this thread's arithmetic -- neither touches other threads' launches
+        with nat.grid_cap(max(1, cus // c) if c > 1 else 0):
+            for j, i in enumerate(rest):
+                s = pool[j % c]
+                with torch.cuda.stream(s), (nat.arithmetic_override('exact') if modes[i] == 'exact'
+                                            else contextlib.nullcontext()):
+                    b = runs[i].greedy_buffers(n_points)
+                    runs[i].greedy_launch(n_points, *b)
+                bufs[i], streams[i] = b, s
     out = []
     for p, v, b, s, mode in zip(runs, views, bufs, streams, modes):
-        if isinstance(mode, tuple):
-            idx = mode[1]
-        else:
-            s.synchronize()
-            idx = b[0].cpu().numpy().view(np.uint32).copy()
-            p.fallback, p.near_tie = None, None
-            if idx.size and int(idx.max()) >= p.n:   # not co-resident next to the others: alone now
-                p.fallback = 'the concurrent launch timed out (grid not co-resident?); re-ran alone'
-                idx, _ = p._greedy_run(n_points, mode)
-            elif mode == 'kernel':
-                with torch.cuda.stream(s):
-                    p.near_tie = nat.near_tie_step(b[2])
-                if p.near_tie != -1:   # flagged: the exact arithmetic decides (p.near_tie keeps the step)
-                    tie = p.near_tie
-                    idx, _ = p._greedy_run(n_points, 'exact')
-                    p.near_tie = tie
+        s.synchronize()
+        idx = b[0].cpu().numpy().view(np.uint32).copy()
+        p.fallback, p.near_tie = None, None
+        if idx.size and int(idx.max()) >= p.n:   # not co-resident next to the others: alone now
+            p.fallback = 'the concurrent launch timed out (grid not co-resident?); re-ran alone'
+            idx, _ = p._greedy_run(n_points, mode)
+        elif mode == 'kernel':
+            with torch.cuda.stream(s):
+                p.near_tie = nat.near_tie_step(b[2])
+            if p.near_tie != -1:   # flagged: the exact arithmetic decides (p.near_tie keeps the step)
+                tie = p.near_tie
+                idx, _ = p._greedy_run(n_points, 'exact')
+                p.near_tie = tie
         out.append(v.to_rows(idx) if v is not None else idx)
     return out

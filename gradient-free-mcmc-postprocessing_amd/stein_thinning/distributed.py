@@ -398,6 +398,11 @@ class PersistentShardedGreedy:
         idx = self.indices() if idx is None else idx
         return bool(idx.size == 0 or int(idx.max()) < self.prob.n)
 
+    def near_tie_step(self) -> int:
+        """This rank's near-tie word of the last run (st_greedy_near_tie: its own rows against the global
+        winner): the first flagged step, -1 none, -2 the run carried no flag."""
+        return nat.near_tie_step(self.ws)
+
     def run(self) -> np.ndarray:
         self.launch()
         return self.indices()
@@ -431,9 +436,34 @@ class ReplicatedGreedy:
         idx = self.indices() if idx is None else idx
         return bool(idx.size == 0 or int(idx.max()) < self.prob.n)
 
+    def near_tie_step(self) -> int:
+        """The single-device kernel's near-tie word of the last run (all rows): see PersistentShardedGreedy."""
+        return nat.near_tie_step(self.ws)
+
     def run(self) -> np.ndarray:
         self.launch()
         return self.indices()
+
+
+_NO_TIE = 1 << 62
+
+
+def combine_near_tie(step: int, group=None) -> int:
+    """Collective: the near-tie verdict of a sharded run from every rank's own word (one all-reduce MIN per
+    thin, none per step).  Each rank's kernel checks its own rows -- everything but the winner and its
+    bitwise duplicates -- against the global winner and the same threshold (bounds over all n rows), so
+    the union of the ranks' flags is the single-device rule (oracle/stein_ref.c sr_greedy_mt_ties).
+    ``step``: this rank's first flagged step, -1 none, -2 no flag computed.  Returns the first flagged step
+    over all ranks, -1 none, -2 if some rank computed no flag (its run must be re-run exactly)."""
+    import torch
+    import torch.distributed as dist
+    v = _NO_TIE if step == -1 else (-1 if step < -1 else int(step))
+    if _world(group)[1] > 1:
+        dev = nat.require_device() if dist.get_backend(group) == 'nccl' else torch.device('cpu')
+        t = torch.tensor([v], dtype=torch.int64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+        v = int(t.item())
+    return -1 if v == _NO_TIE else (-2 if v < 0 else v)
 
 
 # --------------------------------------------------------------------------------------------
@@ -679,13 +709,47 @@ def _thin_sharded_integrand(integrand: SteinIntegrand, n_points: int, group=None
     if world > 1 and not _group_same(np.array([-1 if rows is None else rows.size], dtype=np.int64), group):
         raise ValueError('sharded thin: the ranks disagree on the repeated-row path '
                          '(stein_thinning.set_dedup / ST_DEDUP must agree, and so must the sample)')
-    global last_mode, last_rows_kept
+    global last_mode, last_rows_kept, last_near_tie
     last_rows_kept = None if rows is None else int(rows.size)
-    runner = sharded_runner(integrand, n_points, group, use_graph)
+    runner, last_near_tie = guarded_sharded_run(integrand, n_points, group, use_graph)
     last_mode = runner.mode
     idx = runner.indices()
     return idx if rows is None else rows[idx.astype(np.int64)].astype(np.uint32)
 
 
+def sharded_guard_mode(d: int, world: int) -> Optional[str]:
+    """The near-tie guard of a sharded thin (the single-device rule, DeviceProblem.guard_mode): None when
+    nothing is needed (guard off -- nat.set_near_tie_guard / ST_NEAR_TIE=0 --, the exact arithmetic, or
+    d > 8); 'kernel' for d = 2, 4 on the engines whose kernels flag (persistent device exchange,
+    replicated); 'exact' for the step engines (other d, or ST_SHARDED_EXCHANGE=rccl): their kernels carry
+    no flag, so the thin runs the exact arithmetic -- NumPy's evaluation order -- directly."""
+    if not nat.near_tie_guard() or nat.arithmetic() != 'compact' or d > 8:
+        return None
+    return 'kernel' if exchange_engine(d, world) in ('persistent', 'replicated') else 'exact'
+
+
+def guarded_sharded_run(integrand: SteinIntegrand, n_points: int, group=None, use_graph: bool = True):
+    """Collective: sharded_runner plus the near-tie guard (sharded_guard_mode).  'kernel': after the compact
+    run every rank reads its own word and one all-reduce combines them (combine_near_tie); a flagged run, or
+    one whose engine fell back to kernels without a flag, is run again -- on every rank -- with the exact
+    arithmetic.  Returns (runner, verdict): the verdict is None (no guard), -1 (no step flagged), t >= 0
+    (step t flagged: re-ran exactly) or -2 (ran exactly: no flag available)."""
+    rank, world = _world(group)
+    mode = sharded_guard_mode(integrand.sample.shape[1], world)
+    if mode == 'exact':
+        with nat.arithmetic_override('exact'):
+            return sharded_runner(integrand, n_points, group, use_graph), -2
+    runner = sharded_runner(integrand, n_points, group, use_graph)
+    if mode is None:
+        return runner, None
+    own = runner.near_tie_step() if hasattr(runner, 'near_tie_step') else -2
+    verdict = combine_near_tie(own, group)
+    if verdict == -1:
+        return runner, -1
+    with nat.arithmetic_override('exact'):   # every rank: the verdict is the same on all of them
+        return sharded_runner(integrand, n_points, group, use_graph), verdict
+
+
 last_mode = None   # exchange engine of the last sharded thin in this process (tests / bench)
 last_rows_kept = None   # rows the last sharded thin kept after dropping repeats (None: all)
+last_near_tie = None   # the near-tie verdict of the last sharded thin (guarded_sharded_run)

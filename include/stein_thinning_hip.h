@@ -73,7 +73,7 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * 0 = exact: NumPy's evaluation order rounding for rounding; other pairs are always exact -- see
  * oracle/stein_ref.c and DESIGN.md §3; all ranks of a sharded run must use the same value), key 12 =
  * register rows per thread of the one-device compact-only persistent kernel (4, 6, 8 .. 10; 0 = do
- * not use it; -1 = automatic: from 8 x 512 rows per block 9, or 10 when more than 2048 rows per block
+ * not use it; -1 = automatic: from 8 x 512 rows per block 9 (8 under the near-tie guard), or 10 when more than 2048 rows per block
  * would still be streamed; below that 4 up to 2 560 rows per block, else 6), key 13 = energy-distance kernel variant (0 / -1 = automatic = 1:
  * one partial sum per thread, 4 blocks per CU; 2..5: more partial sums or 8 blocks per CU; 6: the
  * round-2 zero-distance select -- measured alternatives; same distances, sums within
@@ -91,11 +91,14 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * automatic; the per-point sum is reassociated differently, within the 1e-8 tolerance), key 19 =
  * 512-thread persistent kernels: two LDS-row chunks computed as two independent chains (1 / -1 =
  * automatic) or one after the other (0; same results), key 20 = near-tie guard of the compact
- * arithmetic (1 / -1 = on, the default; 0 = off; see st_greedy_near_tie; same indices and sums).
+ * arithmetic (1 / -1 = on, the default; 0 = off; see st_greedy_near_tie; same indices and sums), key 22 = key 11 for the
+ * launches of the CALLING HOST THREAD only (-1 = none: key 11 applies; 0 / 1 as key 11) -- the library keeps
+ * it per thread, so threads thinning side by side (one per GPU) never change each other's arithmetic, key
+ * 23 = key 5 for the calling host thread only (-1 = none; 1..512 blocks).
  */
 int st_tune(int32_t key, int32_t value);
 
-/* the current value of a greedy-kernel st_tune key (0 .. 6, 8 .. 12, 15, 16, 19, 20; -1 = automatic);
+/* the current value of a greedy-kernel st_tune key (0 .. 6, 8 .. 12, 15, 16, 19, 20, 22, 23; -1 = automatic);
  * INT32_MIN for other keys (save / restore around a temporary setting) */
 int32_t st_tune_get(int32_t key);
 
@@ -118,19 +121,21 @@ int st_greedy(const double *x_soa, const double *g_soa, const double *weights, i
               void *stream);
 
 /*
- * Near-tie guard of the compact arithmetic (st_tune key 20).  A guarded run (one device, the compact
- * arithmetic, d = 2 or 4; persistent kernel, batch included) flags the first step t whose selection the
+ * Near-tie guard of the compact arithmetic (st_tune key 20).  A guarded run (the compact arithmetic, d = 2
+ * or 4; persistent kernel, batch and multi-rank included) flags the first step t whose selection the
  * arithmetic could have decided differently from the reference's NumPy evaluation: the smallest running
- * sum of any row other than the winner -- an exact tie included -- within thr(t) of the winner's, thr(t)
- * a bound on how far two rows' sums may move between the compact arithmetic, the exact one and NumPy's
- * (oracle/stein_ref.c sr_greedy_mt_ties states the rule and the bound; the reference's argmin is
- * JAX_Stein_Thinning.ipynb:291-292, np.argmin of the running sums).  Exact ties count, so the guard is
- * meant for problems without adjacent repeated rows (thin the run starts: st_run_starts /
- * st_run_compact).  Reads the workspace of a completed st_greedy / st_greedy_batch problem after
- * synchronising `stream` (the one exception to the enqueue-only rule: a few bytes come back):
- * *step_out = the first flagged step, -1 when none, -2 when the run was not guarded (exact arithmetic,
- * guard off, other d, a multi-rank run, or the launch-per-step kernels).  Callers re-run a flagged thin
- * with the exact arithmetic (st_tune key 11 = 0).
+ * sum of any row other than the winner and the rows equal to it bit for bit (x, g, w: repeated MCMC rows,
+ * adjacent or not, tie in every arithmetic and lose to the lower index on both paths) -- any other exact
+ * tie included -- within thr(t) of the winner's, thr(t) a bound on how far two rows' sums may move between
+ * the compact arithmetic, the exact one and NumPy's (oracle/stein_ref.c sr_greedy_mt_ties states the rule
+ * and the bound; the reference's argmin is JAX_Stein_Thinning.ipynb:291-292, np.argmin of the running
+ * sums).  A multi-rank run (st_greedy_sharded) flags in each rank's workspace the steps its own rows
+ * flag against the global winner (bounds over all n rows): the first flagged step of the thin is the
+ * minimum over the ranks (one all-reduce after the run).  Reads the workspace of a completed st_greedy /
+ * st_greedy_batch / st_greedy_sharded problem after synchronising `stream` (the one exception to the
+ * enqueue-only rule: a few bytes come back): *step_out = the first flagged step, -1 when none, -2 when the
+ * run was not guarded (exact arithmetic, guard off, other d, or the launch-per-step kernels).  Callers
+ * re-run a flagged thin with the exact arithmetic (st_tune key 11 = 0, or key 22 for the calling thread).
  */
 int st_greedy_near_tie(const void *workspace, int64_t workspace_bytes, int64_t *step_out, void *stream);
 

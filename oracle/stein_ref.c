@@ -220,6 +220,16 @@ typedef struct {
 
 typedef struct { mt_ctx *c; int tid; } mt_arg;
 
+/* rows i and j equal bit for bit in x, g (and w): identical pair values in any arithmetic, hence equal
+ * running sums at every step; np.argmin always prefers the lower index, so neither path can tell them
+ * apart (the near-tie rule below does not count such a tie) */
+static int same_row(const mt_ctx *c, int64_t i, int64_t j) {
+    const int d = c->d;
+    if (memcmp(c->x + i * d, c->x + j * d, sizeof(double) * d) != 0) return 0;
+    if (memcmp(c->g + i * d, c->g + j * d, sizeof(double) * d) != 0) return 0;
+    return !c->w || memcmp(c->w + i, c->w + j, sizeof(double)) == 0;
+}
+
 static void *mt_worker(void *p) {
     mt_arg *a = (mt_arg *)p;
     mt_ctx *c = a->c;
@@ -258,12 +268,13 @@ static void *mt_worker(void *p) {
             c->bv[0] = gv;
         }
         pthread_barrier_wait(&c->bar);
-        if (c->gap) {   /* the runner-up: smallest sum of any row other than the winner (ties count) */
+        if (c->gap) {   /* the runner-up: smallest sum of any row other than the winner and its bitwise
+                           duplicates (an exact tie with any other row counts) */
             const double gv = c->bv[0];
             const int64_t wi = c->idx[t];
             double r = INFINITY;
             for (int64_t i = r0; i < r1; i++)
-                if (i != wi && c->A[i] < r) r = c->A[i];
+                if (i != wi && c->A[i] < r && !(c->A[i] == gv && same_row(c, i, wi))) r = c->A[i];
             c->rv[a->tid] = r;
             pthread_barrier_wait(&c->bar);
             if (a->tid == 0) {
@@ -328,11 +339,12 @@ int sr_greedy_mt(const double *x, const double *g, const double *w, int64_t n, i
 }
 
 /*
- * Near-tie guard of the compact arithmetic (the kernels' rule, persistent.hip tie_check): step t (the
- * argmin that gives idx[t]) is flagged when the smallest running sum of any OTHER row -- an exact tie
- * included -- lies within thr(t) of the winner's.  Exact ties count because the guard runs on problems
- * without adjacent repeated rows (the drop-in thins the run starts, device.py dedup_view): two different
- * rows with equal sums tie only by accident of rounding.  thr(t) bounds how far two rows' sums may move
+ * Near-tie guard of the compact arithmetic (the kernels' rule, persistent_kernel.hpp tie_check): step t
+ * (the argmin that gives idx[t]) is flagged when the smallest running sum of any OTHER row -- an exact tie
+ * included -- lies within thr(t) of the winner's, where rows equal to the winner bit for bit (x, g, w: a
+ * repeated MCMC row, adjacent or not) do not count: their sums equal the winner's in every arithmetic and
+ * NumPy resolves them by the lower index exactly as the kernels do.  Any other exact tie counts: two
+ * different rows with equal sums tie only by accident of rounding.  thr(t) bounds how far two rows' sums may move
  * between the compact arithmetic, the exact one and NumPy's evaluation -- diagnostics.py's band (8 ulps
  * per term of the magnitudes a pair value is built from, plus an ulp of the sum per step) for both rows,
  * times 2 -- with ulp(v) <= |v| 2^-52 and the magnitudes bounded by

@@ -103,8 +103,9 @@ def tie_bounds(g, w):
 
 def greedy_ties(x, g, w, l, tr, m, nthreads=None, arith=None, winner_sums=False):
     """greedy_mt plus the kernels' near-tie guard model (stein_ref.c sr_greedy_mt_ties): (idx, A, gap, thr,
-    flagged) where gap[t] = the smallest running sum of any row other than the step-t winner minus the
-    winner's (exact ties count: 0), thr[t] the guard's threshold and flagged[t] = gap[t] <= thr[t] (only
+    flagged) where gap[t] = the smallest running sum of any row other than the step-t winner and its bitwise
+    duplicates minus the winner's (other exact ties count: 0), thr[t] the guard's threshold and
+    flagged[t] = gap[t] <= thr[t] (only
     with the compact arithmetic, d <= 8).  winner_sums=True appends wv[t], the step-t winner's sum."""
     x = np.ascontiguousarray(x, dtype=np.float64)
     g = np.ascontiguousarray(g, dtype=np.float64)

@@ -50,9 +50,11 @@ class CpuShardBackend:
         return _unbits(rec[best, 1]), rec[best, HEADER:]
 
     def step(self, t):
+        from stein_thinning import _native as nat
+        arith = nat.arithmetic()   # the kernels' arithmetic for this thread (an exact re-run included)
         ar = np.arange(self.n)
         if t == 0:
-            A = oracle_c.pairs(self.x, self.g, None, self.l, self.tr, ar, ar)
+            A = oracle_c.pairs(self.x, self.g, None, self.l, self.tr, ar, ar, arith=arith)
             if self.w is not None:
                 A = (A * self.w) * self.w
         else:
@@ -61,7 +63,7 @@ class CpuShardBackend:
             d = self.d
             xs = np.vstack([self.x, row[:d][None]])
             gs = np.vstack([self.g, row[d:2 * d][None]])
-            col = oracle_c.pairs(xs, gs, None, self.l, self.tr, ar, np.full(self.n, self.n))
+            col = oracle_c.pairs(xs, gs, None, self.l, self.tr, ar, np.full(self.n, self.n), arith=arith)
             if self.w is not None:
                 col = (col * self.w) * row[2 * d]
             A = self.A + 2.0 * col

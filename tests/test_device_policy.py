@@ -22,16 +22,25 @@ def test_local_rank_one_process_per_gpu():
 
 
 def test_pool_workers_spread_round_robin():
-    # five joblib workers (the reference's five chains) with consecutive pids on an 8-GPU node
-    got = [nat.select_device_index(8, {}, worker=True, pid=4000 + k) for k in range(5)]
-    assert len(set(got)) == 5
-    # the pool's own worker ordinals (loky / multiprocessing names): an exact round-robin
+    # five joblib workers (the reference's five chains): the pool's own worker ordinals (loky /
+    # multiprocessing / concurrent.futures names) give an exact round-robin
     names = [f'LokyProcess-{k}' for k in range(1, 6)]
     assert [nat.select_device_index(8, {}, worker=True, pid=9, worker_name=nm) for nm in names] == [0, 1, 2, 3, 4]
     assert nat.select_device_index(4, {}, worker=True, pid=9, worker_name='ForkPoolWorker-6') == 1
-    assert nat.select_device_index(4, {}, worker=True, pid=9, worker_name='Dask worker') == 1   # pid 9 % 4
-    assert nat.select_device_index(1, {}, worker=True, pid=4001) is None   # one device: nothing to choose
+    assert nat.select_device_index(4, {}, worker=True, pid=9, worker_name='SpawnProcess-3') == 2
+    # Dask's nanny workers carry no ordinal: their pids spread them
+    got = [nat.select_device_index(8, {}, worker=True, pid=4000 + k, worker_name='Dask Worker process (from Nanny)')
+           for k in range(5)]
+    assert len(set(got)) == 5
+    assert nat.select_device_index(1, {}, worker=True, pid=4001, worker_name='LokyProcess-2') is None   # one device
     assert nat.select_device_index(8, {}, worker=False, pid=4001) is None  # the main process: current device
+
+
+def test_other_child_processes_get_no_policy():
+    """a user's own multiprocessing.Process or a DataLoader worker is not a pool worker -- its
+    device stays the caller's choice (require_device also keeps any non-default device already set)."""
+    for nm in ['Process-3', 'MainProcess', '', 'Dask-like worker 2']:
+        assert nat.select_device_index(8, {}, worker=True, pid=4003, worker_name=nm) is None
 
 
 def test_no_hip_initialisation_at_import():

@@ -11,7 +11,7 @@ import torch.distributed as dist
 import torch.multiprocessing as mp
 
 from oracle import stein_numpy as o
-from stein_thinning.distributed import run_ksd_sharded, run_sharded, shard_bounds, triangle_row_bounds
+from stein_thinning.distributed import combine_near_tie, run_ksd_sharded, run_sharded, shard_bounds, triangle_row_bounds
 
 
 def _free_port():
@@ -186,3 +186,78 @@ def test_triangle_row_bounds_balance():
             assert sum(pairs) == n * (n - 1) // 2
             if n >= 1000:
                 assert max(pairs) - min(pairs) <= 2 * n
+
+
+def rank_first_flag(s, g, w, l, tr, m, r0, r1):
+    """The kernels' near-tie check restricted to one rank's rows [r0, r1) -- what that rank's blocks flag
+    (persistent_kernel.hpp tie_check): per step, the smallest running sum of its rows other than the global
+    winner and the winner's bitwise duplicates, against the global winner's sum and the threshold thr(t)
+    the rank computes from bounds over all n rows.  The first such step, or -1.  (A restatement over the C
+    bit model's sums: test infrastructure.)"""
+    from tests import oracle_c
+    idx, _, _, thr, _, wv = oracle_c.greedy_ties(s, g, w, l, tr, m, winner_sums=True)
+    rows = np.arange(r0, r1)
+    for t in range(m):
+        _, A = oracle_c.greedy(s, g, w, l, tr, t + 1)   # the sums whose argmin is idx[t]
+        j = int(idx[t])
+        dup = np.all(s[rows] == s[j], axis=1) & np.all(g[rows] == g[j], axis=1)
+        same = dup & (np.all(s[rows].view(np.uint64) == s[j].view(np.uint64), axis=1) &
+                      np.all(g[rows].view(np.uint64) == g[j].view(np.uint64), axis=1))
+        if w is not None:
+            same &= w[rows].view(np.uint64) == w[j].view(np.uint64)
+        cand = rows[~same]
+        if cand.size and A[cand].min() - wv[t] <= thr[t]:
+            return t
+    return -1
+
+
+def _tie_data(kind):
+    from tests import margins_ref as mr
+    if kind == 'twins':
+        X, G, _ = mr.near_tie_twins(1)
+    elif kind == 'pooled':
+        X, G, _ = mr.near_tie_twins(6)
+        X, G = np.vstack([X, X]), np.vstack([G, G])
+    else:   # duplicates only: no step is a near tie
+        rng = np.random.default_rng(2)
+        X = rng.normal(size=(300, 2))
+        X, G = np.vstack([X, X[::-1]]), -np.vstack([X, X[::-1]])
+    return X, G
+
+
+def _tie_worker(rank, world, port, kind, out_dir):
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        X, G = _tie_data(kind)
+        s, gs = o._validate_and_standardize(X, G, True)
+        linv = o.make_precon(s, 'id')
+        r0, r1 = shard_bounds(s.shape[0], rank, world)
+        own = rank_first_flag(s, gs, None, linv[0, 0], np.trace(linv), 30, r0, r1)
+        np.save(os.path.join(out_dir, f'tie{rank}.npy'), np.array([own, combine_near_tie(own)]))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize('world,kind', [(2, 'twins'), (3, 'twins'), (2, 'pooled'), (3, 'dups')])
+def test_rank_level_tie_rule_equals_the_model(tmp_path, world, kind):
+    """each rank flags its own rows against the global winner and the global threshold,
+    one all-reduce MIN combines the words (distributed.combine_near_tie); the combined first flagged step
+    equals the single-device model's (oracle/stein_ref.c sr_greedy_mt_ties) on near-tie twins, twins pooled
+    with their own copy (the winners' duplicates in other shards must not flag) and duplicates only."""
+    from tests import oracle_c
+    mp.spawn(_tie_worker, args=(world, _free_port(), kind, str(tmp_path)), nprocs=world, join=True)
+    X, G = _tie_data(kind)
+    s, gs = o._validate_and_standardize(X, G, True)
+    linv = o.make_precon(s, 'id')
+    *_, flagged = oracle_c.greedy_ties(s, gs, None, linv[0, 0], np.trace(linv), 30)
+    want = int(np.flatnonzero(flagged)[0]) if flagged.any() else -1
+    got = [np.load(tmp_path / f'tie{r}.npy') for r in range(world)]
+    assert all(int(v[1]) == want for v in got)
+    assert min((int(v[0]) for v in got if v[0] >= 0), default=-1) == want
+    if kind == 'dups':
+        assert want == -1
+
+
+def test_combine_near_tie_single_process():
+    assert combine_near_tie(-1) == -1 and combine_near_tie(7) == 7 and combine_near_tie(-2) == -2

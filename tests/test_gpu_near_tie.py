@@ -130,18 +130,83 @@ def test_thin_chains_guarded():
         np.testing.assert_array_equal(idx, o.thin(X, G, 30))
 
 
-def test_config2_run_starts_unflagged():
-    """Config 2 through the drop-in path: the run starts are thinned (the guard counts exact ties), no step
-    is flagged, and the indices equal the plain full thin's."""
+@pytest.mark.parametrize('dedup', ['always', False])
+def test_config2_unflagged_run_starts_and_raw_rows(dedup):
+    """Config 2 through the guarded path, on its run starts and on all 2e5 raw rows (~77 % repeats, every
+    winner tied exactly by its own repeats): no step is flagged -- ties between rows equal bit for bit do not
+    count (VERDICT r05 next #2) -- and the indices equal the plain full thin's."""
     import bench
     cfg = dict(bench.CONFIGS['c2'])
     integrand, _, _ = bench.make_integrand(cfg)
     prob = integrand.device_problem()
-    got = prob.greedy(cfg["m"], dedup=True, guard=True)
-    assert prob.dedup_used and prob.near_tie == -1
+    got = prob.greedy(cfg["m"], dedup=dedup, guard=True)
+    assert prob.dedup_used == bool(dedup) and prob.near_tie == -1
     full, _ = oc.greedy_mt(integrand.sample, integrand.gradient, None, integrand.linv_scale, integrand.linv_trace,
                            cfg['m'])
     np.testing.assert_array_equal(got, full)
+
+
+def _pooled_permuted(n=50_000, seed=4):
+    """A bivariate sample pooled with an identical copy and shuffled: every row has a bitwise duplicate far
+    from it (two identical chains pooled, then permuted -- nothing adjacent for dedup_view to drop)."""
+    from oracle import models
+    X, G = models.bivariate_reference_sample(n)[:2]
+    p = np.random.default_rng(seed).permutation(2 * n)
+    return np.vstack([X, X])[p], np.vstack([G, G])[p]
+
+
+def test_non_adjacent_duplicates_take_no_exact_rerun():
+    """The default thin() on a sample whose duplicates are all non-adjacent: the guarded kernel sees the
+    winner tied exactly by its duplicate at every step and flags nothing, so no exact re-run happens; the
+    indices are the NumPy path's (VERDICT r05 next #2)."""
+    X, G = _pooled_permuted()
+    want = o.thin(X, G, 30)
+    integrand = st._make_stein_integrand(X, G)
+    got = st._greedy_search(30, integrand)
+    prob = integrand.device_problem()
+    assert not prob.dedup_used and prob.near_tie == -1   # guarded, unflagged: no re-run
+    np.testing.assert_array_equal(got, want)
+    _, step, _ = _compact_run(prob, 30)
+    assert step == -1
+
+
+def test_duplicated_near_ties_flag_like_the_model():
+    """Near-tie twins in a sample pooled with its own copy: the twins still flag (a twin is not a bitwise
+    duplicate of the winner), the winners' exact copies do not; first flagged step, bounds and final
+    threshold state equal the bit model's, and the default thin returns NumPy's indices."""
+    X, G, steps = mr.near_tie_twins(2)
+    X2, G2 = np.vstack([X, X]), np.vstack([G, G])
+    integrand = st._make_stein_integrand(X2, G2)
+    prob = integrand.device_problem()
+    idx, step, state = _compact_run(prob, 30)
+    midx, _, _, _, flagged, wv = oc.greedy_ties(integrand.sample, integrand.gradient, None, integrand.linv_scale,
+                                                integrand.linv_trace, 30, winner_sums=True)
+    np.testing.assert_array_equal(idx, midx)
+    assert step == np.flatnonzero(flagged)[0] == steps[0]
+    thr_all, Q, E = model_thresholds(integrand.gradient, None, integrand.linv_scale, integrand.linv_trace, midx, wv)
+    np.testing.assert_array_equal(state, list(oc.tie_bounds(integrand.gradient, None)) + [Q, E, thr_all[-1]])
+    np.testing.assert_array_equal(stein_thinning.thin(X2, G2, 30), o.thin(X2, G2, 30))
+
+
+def test_exact_tie_between_different_rows_flags_on_the_gpu():
+    """rows r and -r (score -x) tie exactly at step 0 without being duplicates: flagged at step 0, as the
+    model (tests/test_near_tie_cpu.py) says."""
+    rng = np.random.default_rng(8)
+    X = rng.normal(size=(300, 2))
+    X = X[np.sum(X * X, axis=1) > 0.5]
+    X[3] = [0.125, -0.25]
+    X[200] = -X[3]
+    integrand = st._make_stein_integrand(X, -X, standardize=False)
+    idx, step, _ = _compact_run(integrand.device_problem(), 3)
+    assert idx[0] == 3 and step == 0
+
+
+def test_thin_chains_one_near_tie_chain():
+    """ADVICE r05: thin_chains with a single chain (greedy_concurrent's one-at-a-time branch, also what a
+    GPU with one chain of a spread runs) keeps the guard: the twins' chain returns NumPy's indices."""
+    X, G, _ = mr.near_tie_twins(0)
+    got = stein_thinning.thin_chains([X], [G], 30)
+    np.testing.assert_array_equal(got[0], o.thin(X, G, 30))
 
 
 @pytest.mark.parametrize('n', [100_000, 300_000, 600_000])
