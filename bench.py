@@ -149,16 +149,12 @@ def _persistent_nt(n_shard: int, d: int) -> int:
 def _persistent_label(n_shard: int, d: int, gf: bool, arithmetic: str, world: int) -> str:
     """The persistent kernel launch_greedy_persistent enqueues by default (persistent.hip): one device,
     512-thread blocks and at least 4 096 rows per block under the compact arithmetic -> the
-    compact-only kernel (9 register rows per thread, 10 when more than 2 048 rows per block would
-    still be streamed) with the general kernel gated behind it."""
+    compact-only kernel (9 register rows per thread) with the general kernel gated behind it."""
     nt = _persistent_nt(n_shard, d)
     rows = -(-n_shard // 256)
     g = str(gf).lower()
     if world == 1 and nt == 512 and arithmetic == 'compact' and rows >= 8 * 512:
-        row_bytes = (2 * d + 1 + (1 if gf else 0)) * 8
-        rl_cap = (163840 - 1024 - 256) // row_bytes // 64 * 64
-        rt = 10 if rows - 9 * 512 - rl_cap > 2048 else 9
-        return (f'greedy_persistent<{d},{g},{rt},512,1,compact,compact-only> (+ the general kernel gated behind '
+        return (f'greedy_persistent<{d},{g},9,512,1,compact,compact-only> (+ the general kernel gated behind '
                 f'it: returns at once)')
     return f'greedy_persistent<{d},{g},RT,{nt}>'
 
@@ -432,10 +428,16 @@ def chains_over_gpus(rank: int, world: int, dev, chains: int = 5, reps: int = 3)
     probs = {c: st._make_stein_integrand(*data[c], preconditioner='med').device_problem() for c in mine}
     guard = nat.near_tie_guard()
 
+    import contextlib
+    # rehearsal (ranks sharing one GPU): each rank's batch grid within its 256 / world CUs, so the ranks'
+    # persistent grids co-reside
+    share = nat.grid_cap(max(1, 256 // world // max(1, len(mine)))) if SHARE_DEVICE else contextlib.nullcontext()
+
     def run_mine():
         for p in probs.values():
             p._dedup = False   # run detection inside the timed region
-        return sdev.greedy_concurrent([probs[c] for c in mine], m, dedup=True, guard=guard) if mine else []
+        with share:
+            return sdev.greedy_concurrent([probs[c] for c in mine], m, dedup=True, guard=guard) if mine else []
     got = dict(zip(mine, run_mine()))   # warm-up
     times = []
     for _ in range(reps):
@@ -562,6 +564,7 @@ def main():
     ap.add_argument('--cpu-steps', type=int, default=100, help='greedy steps of the NumPy one-core sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-kernel-timing', action='store_true')
+    ap.add_argument('--no-e2e', action='store_true', help='skip the end_to_end legs (drop-in thin on host arrays)')
     ap.add_argument('--no-graph', action='store_true', help='N > 1: eager per-step launches instead of a HIP graph')
     ap.add_argument('--sharded', action='store_true', help='use the sharded (RCCL) path even at N = 1')
     ap.add_argument('--no-config5', action='store_true',
@@ -833,7 +836,7 @@ def main():
         if world == 1 and not sharded:
             dedup = dedup_timing(prob, m, result_idx, stream)
         e2e = None
-        if world == 1 and not cfg['gf'] and not cfg.get('d50'):
+        if world == 1 and not cfg['gf'] and not cfg.get('d50') and not args.no_e2e:
             # the drop-in call on host arrays (not `value`): standardisation + 'med' + H2D upload +
             # SoA layout + the persistent launch + D2H of the indices
             from stein_thinning import thinning as st

@@ -14,8 +14,6 @@ namespace st {
 const void* guarded_persistent_fn(int d, bool gf, int rt, int nt, int bpc, bool gen, bool batch);
 // the small-shard instantiations (persistent_small.hip: 256 threads, 1 / 2 register rows), or nullptr
 const void* small_persistent_fn(int d, bool gf, int rt, bool cmp, bool batch, bool guard);
-// the mid-size compact-only instantiations (persistent_cmp.hip: 512 threads, 4 / 6 register rows), or nullptr
-const void* cmp_persistent_fn(int d, bool gf, int rt, bool batch, bool guard);
 
 int64_t persistent_rep_stride(int G, int rec_stride, int nrep) {
     const int64_t one = (int64_t)G * rec_stride;
@@ -48,10 +46,9 @@ static int g_persist_grid = -1; // st_tune key 5: grid cap (blocks), -1 auto (on
 // threads thinning side by side never change each other's grids
 static thread_local int t_persist_grid = -1;
 static int grid_cap() { return t_persist_grid > 0 ? t_persist_grid : g_persist_grid; }
-static int g_persist_bpc = -1;  // st_tune key 8: blocks per CU (1, 2), -1 auto
 static int g_persist_pitch = -1; // st_tune key 9: record pitch in bytes (16 .. 4096, power of 2), -1 auto
 static int g_persist_nrep = -1;  // st_tune key 10: record replicas (1 .. 32, power of 2), -1 auto
-static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register rows (4, 6, 8 .. 10), 0 off, -1 auto
+static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register rows (8, 9), 0 off, -1 auto
 // st_tune key 15: the 512-thread kernels keep the streamed rows' running sums in LDS (1) or in HBM (0,
 // the default).  Measured (round 4, same box, config 4, profiles/r04_streamed_sums_lds_rejected.log):
 // PMC WRITE_SIZE 1.08 GB -> 0.15 GB per thin, but 6.82 -> 6.94-7.01 ms: the 8 B per streamed row take
@@ -74,12 +71,11 @@ static int g_persist_delay = -1;
 // measured and dropped: the extra live registers spilled inside the step loop (75 VGPRs of scratch)
 // and every variant ran at 8.6-8.7 ms (profiles/r04_lds_interleaved_rejected.log)
 static int g_persist_lds2 = -1;
-// automatic register rows of the compact-only kernel: 9 (28 B of scratch at d = 4) unless more than
-// kCmpStreamRows rows per block would still be streamed, then 10 (108 B of scratch; the streamed
-// rows then no longer stay in the XCD's L2).  Same-box, d = 4, m = 1000 (profiles/r03_compact_only_rt.log):
-// n = 2e6: 7.81 (general kernel) / 7.76 (8) / 7.05 (9) / 7.29 (10) us per step; n = 3e6: 19.8 /
-// 19.7 / 18.5 / 17.8.
-constexpr int64_t kCmpStreamRows = 2048;
+// automatic register rows of the compact-only kernel: 9 (28 B of scratch at d = 4; 8 under the near-tie
+// guard).  Same-box, d = 4, m = 1000 (profiles/r03_compact_only_rt.log): n = 2e6: 7.81 (general kernel) /
+// 7.76 (8) / 7.05 (9) us per step.  (Round 6 pruned the 10-row plan -- 17.8 against 18.5 us per step at
+// n = 3e6 only, no BASELINE config -- with the other families that won nothing on a BASELINE config or the
+// LV call: DESIGN.md section 4, "Plans".)
 static uint64_t* g_stamps = nullptr;
 #ifdef ST_PERSIST_STAMPS
 extern "C" int st_debug_set_stamps(uint64_t* buf) { g_stamps = buf; return 0; }
@@ -91,7 +87,6 @@ int persistent_tune_get(int key) {
         case 4: return g_persist_nt;
         case 5: return g_persist_grid;
         case 23: return t_persist_grid;
-        case 8: return g_persist_bpc;
         case 9: return g_persist_pitch;
         case 10: return g_persist_nrep;
         case 12: return g_persist_cmp;
@@ -104,7 +99,7 @@ int persistent_tune_get(int key) {
 
 int persistent_tune(int key, int value) {
     if (key == 3) {
-        if (value < -1 || value > 64) return -1;
+        if (value != -1 && value != 0 && value != 1 && value != 2 && value != 4 && value != 8 && value != 16) return -1;
         g_persist_rt = value;
         return 0;
     }
@@ -123,10 +118,8 @@ int persistent_tune(int key, int value) {
         t_persist_grid = value;
         return 0;
     }
-    if (key == 8) {
-        if (value != -1 && value != 1 && value != 2) return -1;
-        g_persist_bpc = value;
-        return 0;
+    if (key == 8) {   // blocks per CU: one (two-block plans pruned in round 6)
+        return value == -1 || value == 1 ? 0 : -1;
     }
     if (key == 9) {
         if (value != -1 && (value < 16 || value > 4096 || (value & (value - 1)))) return -1;
@@ -139,7 +132,7 @@ int persistent_tune(int key, int value) {
         return 0;
     }
     if (key == 12) {
-        if (value != -1 && value != 0 && value != 4 && value != 6 && (value < 8 || value > 10)) return -1;
+        if (value != -1 && value != 0 && value != 8 && value != 9) return -1;
         g_persist_cmp = value;
         return 0;
     }
@@ -174,10 +167,6 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     if constexpr (RT < 4 && D <= kMaxCtDim) {   // small shards: compiled in persistent_small.hip
         static_assert(NT == 256 && BPC == 1 && GEN, "small-shard plans only");
         fn = small_persistent_fn(D, GF, RT, arith_compact(), b != nullptr, guarded);
-        if (!fn) return hipErrorNotSupported;
-    } else if constexpr (!GEN && RT < 8) {   // mid-size compact-only: compiled in persistent_cmp.hip
-        static_assert(NT == 512 && BPC == 1, "mid-size compact-only plans only");
-        fn = cmp_persistent_fn(D, GF, RT, b != nullptr, guarded);
         if (!fn) return hipErrorNotSupported;
     } else if (guarded) {
         if constexpr (D <= kMaxCtDim) {
@@ -226,36 +215,27 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     return hipLaunchKernel(fn, dim3(G), dim3(NT), kargs, lds, s);
 }
 
-// compact-only kernels: 512-thread blocks, 4 / 6 / 8 / 9 / 10 register rows per thread
+// compact-only kernels: 512-thread blocks, 8 / 9 register rows per thread
 template <int D, bool GF>
 static hipError_t launch_p_cmp(const PersistArgs& a, int rt, int G, size_t lds, hipStream_t s, bool dry,
                                const BatchArgs* b) {
-    if (rt >= 10) return launch_p<D, GF, 10, 512, 1, false>(a, G, lds, s, dry, b);
     if (rt == 9) return launch_p<D, GF, 9, 512, 1, false>(a, G, lds, s, dry, b);
-    if (rt <= 4) return launch_p<D, GF, 4, 512, 1, false>(a, G, lds, s, dry, b);
-    if (rt <= 6) return launch_p<D, GF, 6, 512, 1, false>(a, G, lds, s, dry, b);
     return launch_p<D, GF, 8, 512, 1, false>(a, G, lds, s, dry, b);
 }
 
+// the plans ("Plans"): 512-thread blocks with 4 / 8 register rows, 256-thread blocks with
+// 1 / 2 (persistent_small.hip) / 4
 template <int D, bool GF>
-static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int bpc, int G, size_t lds, hipStream_t s,
+static hipError_t launch_p_rt(const PersistArgs& a, int rt, int nt, int G, size_t lds, hipStream_t s,
                                bool dry, const BatchArgs* b) {
-    if (bpc == 2) {
-        if (b) return hipErrorNotSupported;
-        if (rt <= 4) return launch_p<D, GF, 4, 256, 2>(a, G, lds, s, dry);
-        return launch_p<D, GF, 8, 256, 2>(a, G, lds, s, dry);
-    }
     if (nt == 512) {
         if (rt <= 4) return launch_p<D, GF, 4, 512>(a, G, lds, s, dry, b);
-        if (rt <= 6) return launch_p<D, GF, 6, 512>(a, G, lds, s, dry, b);
         return launch_p<D, GF, 8, 512>(a, G, lds, s, dry, b);
     }
     switch (rt) {
         case 1: return launch_p<D, GF, 1, 256>(a, G, lds, s, dry, b);
         case 2: return launch_p<D, GF, 2, 256>(a, G, lds, s, dry, b);
-        case 4: return launch_p<D, GF, 4, 256>(a, G, lds, s, dry, b);
-        case 8: return launch_p<D, GF, 8, 256>(a, G, lds, s, dry, b);
-        default: return launch_p<D, GF, 16, 256>(a, G, lds, s, dry, b);
+        default: return launch_p<D, GF, 4, 256>(a, G, lds, s, dry, b);
     }
 }
 
@@ -265,14 +245,14 @@ static hipError_t launch_cmp(const PersistArgs& a, int d, bool gf, int rt, int G
     return gf ? launch_p_cmp<4, true>(a, rt, G, lds, s, dry, b) : launch_p_cmp<4, false>(a, rt, G, lds, s, dry, b);
 }
 
-static hipError_t launch_kind(const PersistArgs& a, int d, bool wide, bool gf, int rt, int nt, int bpc, int G,
+static hipError_t launch_kind(const PersistArgs& a, int d, bool wide, bool gf, int rt, int nt, int G,
                               size_t lds, hipStream_t s, bool dry, const BatchArgs* b = nullptr) {
     if (wide) {
         if (b) return hipErrorNotSupported;
         return gf ? launch_p<kWideD, true, 1, 256>(a, G, lds, s, dry) : launch_p<kWideD, false, 1, 256>(a, G, lds, s, dry);
     }
-    if (d == 2) return gf ? launch_p_rt<2, true>(a, rt, nt, bpc, G, lds, s, dry, b) : launch_p_rt<2, false>(a, rt, nt, bpc, G, lds, s, dry, b);
-    return gf ? launch_p_rt<4, true>(a, rt, nt, bpc, G, lds, s, dry, b) : launch_p_rt<4, false>(a, rt, nt, bpc, G, lds, s, dry, b);
+    if (d == 2) return gf ? launch_p_rt<2, true>(a, rt, nt, G, lds, s, dry, b) : launch_p_rt<2, false>(a, rt, nt, G, lds, s, dry, b);
+    return gf ? launch_p_rt<4, true>(a, rt, nt, G, lds, s, dry, b) : launch_p_rt<4, false>(a, rt, nt, G, lds, s, dry, b);
 }
 
 namespace {
@@ -280,7 +260,7 @@ namespace {
 struct Plan {
     PersistArgs a, ac;     // general kernel / compact-only kernel (use_cmp)
     bool wide, gf, use_cmp, own_region;
-    int d, rt, nt, bpc, G, rt_c;
+    int d, rt, nt, G, rt_c;
     size_t lds, lds_c;
     int64_t region;        // bytes of one record region
     char* ws;
@@ -316,8 +296,7 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
         lds_max = lds_optin;
     if (lds_max > 163840) lds_max = 163840;
     int nt = wide ? 256 : (g_persist_nt > 0 ? g_persist_nt : 256);
-    const int bpc = (!wide && nt == 256 && g_persist_bpc == 2) ? 2 : 1;
-    int G = cus * bpc > kMaxGrid ? kMaxGrid : cus * bpc;
+    int G = cus > kMaxGrid ? kMaxGrid : cus;   // one block per CU
     if (grid_cap > 0 && G > grid_cap) G = grid_cap;
     const int64_t min_rows = 256;   // fewer blocks for small n: exchange cost grows with G
     if (n_shard < (int64_t)G * min_rows) G = (int)((n_shard + min_rows - 1) / min_rows);
@@ -341,14 +320,15 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     // auto: 512-thread blocks (two waves per SIMD, dynamic chunks) once a block has more rows than
     // one wave per SIMD keeps in registers comfortably (measured crossover 1e3 .. 2e3 rows per CU,
     // scripts/sweep_nt_crossover.sh)
-    if (!wide && g_persist_nt <= 0 && bpc == 1 && R > kNt512MinRows) nt = 512;
-    const int rt_max = (nt == 512 || bpc == 2) ? 8 : 16;
+    if (!wide && g_persist_nt <= 0 && R > kNt512MinRows) nt = 512;
+    // register rows per thread: 512-thread blocks 8, or 4 when 8 would leave register slots empty;
+    // 256-thread blocks 4 (st_tune key 3 may ask for fewer, or for 4 on 512 threads)
+    const int rt_max = nt == 512 ? 8 : 4;
     int rt = rt_force > 0 ? rt_force : (g_persist_rt > 0 ? g_persist_rt : rt_max);
-    const bool small_ok = nt == 256 && bpc == 1 && !wide;   // 1 / 2 register rows: persistent_small.hip
-    if (rt != 4 && rt != 6 && rt != 8 && rt != 16 && !(small_ok && (rt == 1 || rt == 2))) rt = rt_max;
+    const bool small_ok = nt == 256 && !wide;   // 1 / 2 register rows: persistent_small.hip
+    if (rt != 4 && rt != 8 && !(small_ok && (rt == 1 || rt == 2))) rt = rt_max;
     if (rt > rt_max) rt = rt_max;
-    if (rt == 6 && (nt != 512 || bpc == 2)) rt = 8;
-    while (rt > 4 && (int64_t)rt * nt > R) rt = rt == 6 ? 4 : rt / 2;   // no empty register rows
+    if (rt == 8 && (int64_t)rt * nt > R) rt = 4;   // no empty register rows
     // small shards: the fewest register rows that hold the block's rows (padding rows compute like real
     // ones; 1 / 2 rows per thread at <= 256 / 512 rows per block)
     if (small_ok && g_persist_rt <= 0 && rt_force <= 0 && R <= 2 * 256) rt = R <= 256 ? 1 : 2;
@@ -361,16 +341,17 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     // (the 256-thread guarded kernels also hold every thread's step record, GuardLanes)
     const size_t head = (sizeof(Scratch) + 15) / 16 * 16 + (guard ? (sizeof(GuardScratch) + 15) / 16 * 16 : 0) +
                         (guard && nt != 512 ? (sizeof(GuardLanes) + 15) / 16 * 16 : 0);
-    const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) / bpc - 1024;   // static + slack
+    const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) - 1024;   // static + slack
     // LDS rows (whole 64-row chunks) for rows past the register rows; the 512-thread (dynamic-chunk)
     // kernels also keep every streamed row's running sum in LDS (8 B per row, whole chunks)
     // (st_tune key 15 = 1 only; when the streamed sums alone would not fit -- more than ~20 000
     // streamed rows per block -- they stay in HBM: sal = 0)
     auto lds_rows = [&](int nt_, int rt_, int64_t& rl, size_t& bytes, int& sal) {
         const int64_t need_ = R - (int64_t)rt_ * nt_;
-        sal = g_persist_sal == 1 && nt_ == 512 && bpc == 1 && need_ > 0 &&
+        sal = g_persist_sal == 1 && nt_ == 512 && need_ > 0 &&
               head + (size_t)(need_ + 63) / 64 * 64 * sizeof(double) <= budget;
         rl = need_ > 0 ? need_ / 64 * 64 : 0;
+        if (guard && rl > kGuardLdsRows) rl = kGuardLdsRows;   // the guard's repeat bits (GuardScratch::lrep)
         auto total = [&](int64_t l) {
             const int64_t st = need_ - l > 0 ? (need_ - l + 63) / 64 * 64 : 0;
             return head + (size_t)l * row_bytes + (sal ? (size_t)st * sizeof(double) : 0);
@@ -390,7 +371,7 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     char* p = static_cast<char*>(ws);
     PersistArgs a{};
     if (plan_only) {   // eligibility query (st_greedy_sharded_supported): everything but the launch
-        hipError_t e = launch_kind(a, d, wide, gf, rt, nt, bpc, G, lds, s, true);
+        hipError_t e = launch_kind(a, d, wide, gf, rt, nt, G, lds, s, true);
         if (e == hipSuccess) *used = 1;
         return e;
     }
@@ -427,24 +408,16 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     bool use_cmp = false;
     int rt_c = 0;
     size_t lds_c = 0;
-    // (round 5: a single launch from 1 280 rows per block, every 512-thread plan -- below 8 x 512 rows with
-    // 4 or 6 register rows, where the general kernel keeps 4 and the rest in LDS: the LV call -1 %; a batch of such blocks gained nothing (the LV chains: within noise,
-    // 5 % slower in a first A/B), so a batch keeps the 8 x 512 floor -- profiles/r05_mid_compact_ab.log)
-    if (rs->nranks == 1 && arith_compact() && nt == 512 && bpc == 1 && !wide && g_persist_cmp != 0 &&
-        (!batch || R >= 8 * 512 || cmp_force > 0 || g_persist_cmp > 0)) {
-        const int64_t rl_cap = (int64_t)((budget - head) / row_bytes) / 64 * 64;
+    // (round 5's mid-size compact-only plans -- 4 / 6 register rows from 1 280 rows per block -- gained 1.5 % on
+    // the LV call and nothing on a BASELINE config; pruned in round 6 with the other families below the 3 % bar)
+    if (rs->nranks == 1 && arith_compact() && nt == 512 && !wide && g_persist_cmp != 0 && R >= 8 * 512) {
         if (cmp_force > 0)
             rt_c = cmp_force;   // a batch's common register rows (launch_greedy_persistent_batch)
-        else if (R >= 8 * 512)
-            rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R - 9 * 512 - rl_cap > kCmpStreamRows ? 10 : 9);
         else
-            // empty register slots are swept like full ones, LDS rows cost ~1.7 register rows: 4 up to
-            // 5 x 512 rows, then 6 (profiles/r05_mid_rows_probe.log: 8 never won below 8 x 512)
-            rt_c = g_persist_cmp > 0 ? g_persist_cmp : (R <= 5 * 512 ? 4 : 6);
-        while (cmp_force <= 0 && rt_c > 8 && (int64_t)rt_c * 512 > R) --rt_c;   // no empty register rows
-        // guarded: at most 8 register rows -- the guard's rescans take the registers a ninth row needs (9 / 10
-        // rows spill inside the step loop: +38 % at config 4 in round 5; 8 rows keep the sweep spill-free)
-        if (guard && rt_c > 8) rt_c = 8;
+            rt_c = g_persist_cmp > 0 ? g_persist_cmp : 9;
+        // guarded: 8 register rows -- the guard's rescans take the registers a ninth row needs (9 rows spill
+        // inside the step loop; st_tune key 12 = 9 still selects 9)
+        if (guard && rt_c > 8 && g_persist_cmp <= 0 && cmp_force <= 0) rt_c = 8;
         int64_t RLc = 0;
         int salc = 0;
         lds_rows(512, rt_c, RLc, lds_c, salc);
@@ -464,7 +437,7 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     P.ac = ac;
     P.wide = wide; P.gf = gf; P.use_cmp = use_cmp;
     P.own_region = use_cmp && kWsControlBytes + 2 * region <= ws_bytes;
-    P.d = d; P.rt = rt; P.nt = nt; P.bpc = bpc; P.G = G; P.rt_c = rt_c;
+    P.d = d; P.rt = rt; P.nt = nt; P.G = G; P.rt_c = rt_c;
     P.lds = lds; P.lds_c = lds_c;
     P.region = region;
     P.ws = p;
@@ -540,7 +513,7 @@ hipError_t launch_greedy_persistent(const double* x, const double* g, const doub
         if (!P.own_region && (e = hipMemsetAsync(P.ws + kWsControlBytes, 0, (size_t)P.region, s)) != hipSuccess)
             return e;
     }
-    e = launch_kind(P.a, P.d, P.wide, P.gf, P.rt, P.nt, P.bpc, P.G, P.lds, s, false);
+    e = launch_kind(P.a, P.d, P.wide, P.gf, P.rt, P.nt, P.G, P.lds, s, false);
     if (e == hipSuccess) *used = 1;
     return e;
 }
@@ -579,7 +552,7 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
                                            cap, P[q], rt_force, cmp_force, true);
             if (e != hipSuccess) return e;
             const Plan& p0 = P[0];
-            if (P[q].wide || P[q].nt != p0.nt || P[q].bpc != 1 || P[q].gf != p0.gf || P[q].use_cmp != p0.use_cmp)
+            if (P[q].wide || P[q].nt != p0.nt || P[q].gf != p0.gf || P[q].use_cmp != p0.use_cmp)
                 return hipErrorNotSupported;
             rt_max_seen = std::max(rt_max_seen, P[q].rt);
             rtc_max_seen = std::max(rtc_max_seen, P[q].rt_c);
@@ -604,7 +577,7 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
     const int G = bc.blk_begin[count];
     const Plan& p0 = P[0];
     // residency and the kernel's existence for this combination, before anything is enqueued
-    if (launch_kind(p0.a, d, false, p0.gf, p0.rt, p0.nt, 1, G, lds, s, true, &bg) != hipSuccess ||
+    if (launch_kind(p0.a, d, false, p0.gf, p0.rt, p0.nt, G, lds, s, true, &bg) != hipSuccess ||
         (p0.use_cmp && launch_cmp(p0.ac, d, p0.gf, p0.rt_c, G, lds_c, s, true, &bc) != hipSuccess))
         return hipErrorNotSupported;
     hipError_t e;
@@ -620,7 +593,7 @@ hipError_t launch_greedy_persistent_batch(int count, const BatchProblem* pr, int
                 (e = hipMemsetAsync(P[q].ws + kWsControlBytes, 0, (size_t)P[q].region, s)) != hipSuccess)
                 return e;
     }
-    e = launch_kind(p0.a, d, false, p0.gf, p0.rt, p0.nt, 1, G, lds, s, false, &bg);
+    e = launch_kind(p0.a, d, false, p0.gf, p0.rt, p0.nt, G, lds, s, false, &bg);
     if (e == hipSuccess) *used = 1;
     return e;
 }

@@ -21,24 +21,16 @@ const void* kernel(bool batch) {
 // the plans launch_p instantiates (persistent.hip launch_p_cmp / launch_p_rt), compact arithmetic
 template <int D, bool GF>
 const void* pick(int rt, int nt, int bpc, bool gen, bool batch) {
-    if (!gen) {   // compact-only kernels: 512 threads, 8 register rows (guarded plans use no more: persistent.hip)
-        if (nt != 512 || bpc != 1 || rt != 8) return nullptr;
-        return kernel<D, GF, 8, 512, 1, false>(batch);
-    }
-    if (bpc == 2) {
-        if (rt <= 4) return kernel<D, GF, 4, 256, 2, true>(batch);
-        return kernel<D, GF, 8, 256, 2, true>(batch);
+    if (bpc != 1) return nullptr;
+    if (!gen) {   // compact-only kernels: 512 threads, 8 register rows (9 only when st_tune key 12 asks: persistent.hip)
+        if (nt != 512 || rt < 8 || rt > 9) return nullptr;
+        return rt == 9 ? kernel<D, GF, 9, 512, 1, false>(batch) : kernel<D, GF, 8, 512, 1, false>(batch);
     }
     if (nt == 512) {
         if (rt <= 4) return kernel<D, GF, 4, 512, 1, true>(batch);
-        if (rt <= 6) return kernel<D, GF, 6, 512, 1, true>(batch);
         return kernel<D, GF, 8, 512, 1, true>(batch);
     }
-    switch (rt) {
-        case 4: return kernel<D, GF, 4, 256, 1, true>(batch);
-        case 8: return kernel<D, GF, 8, 256, 1, true>(batch);
-        default: return kernel<D, GF, 16, 256, 1, true>(batch);
-    }
+    return rt == 4 ? kernel<D, GF, 4, 256, 1, true>(batch) : nullptr;   // (1 / 2 rows: persistent_small.hip)
 }
 
 }  // namespace

@@ -66,6 +66,8 @@ struct Scratch {          // small per-block scratch at the start of the dynamic
 // the rescan's smallest sum of the block's rows other than the block's minimum row and its bitwise
 // duplicates ("other"); the step's winner (row and sum; tie_check reads its score row and weight from the
 // inputs) and this block's published minimum and its row; the threshold recurrence
+// LDS rows a guarded plan keeps at most (the repeat bits of GuardScratch::lrep; persistent.hip caps RL)
+constexpr int kGuardLdsRows = 4096;
 struct GuardScratch {
     double rs_o[2][kMaxPWaves];
     uint32_t win_i[2], blk_i[2];
@@ -77,6 +79,8 @@ struct GuardScratch {
     // minimum -- finished (duplicate test) and reduced by wave 1 after publishing step t, off the critical path
     double w0_o[64];
     uint32_t w0_m[64];
+    // LDS rows that repeat their predecessor row bit for bit (x, g, w): bit e of the LDS rows (staging)
+    uint32_t lrep[kGuardLdsRows / 32];
     int tied;             // a step was flagged (this block's word was written)
 };
 
@@ -248,7 +252,7 @@ struct PersistArgs {
 // Diagnostic build (-DST_PERSIST_STAMPS, tools/probe only; never the product library): lane 0 of
 // every block records s_memrealtime (100 MHz, chip-wide clock) at each phase of steps
 // [kStampFirst, kStampFirst + kStampSteps).
-[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 24;
+[[maybe_unused]] constexpr int kStampFirst = 20, kStampSteps = 32, kStampPhases = 32;
 #ifdef ST_PERSIST_STAMPS
 #define ST_STAMP(a, t, ph)                                                                         \
     do {                                                                                            \
@@ -349,15 +353,15 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
             combine_waves<NT>(sc, k, ib);
             const double vb = key_value(k);
             sc->vblk = vb;   // read by every thread after wait_and_pick's barrier
-            if constexpr (GUARD) {   // this block's minimum of step t and its row
-                gsc->blk_v[t & 1] = vb;
-                gsc->blk_i[t & 1] = ib;
-            }
             uint64_t* gr = a.gran + (t & 1) * a.rep_stride + (int64_t)bid * a.rec_stride;
             const uint64_t tag = step_tag(t);
             __hip_atomic_store(gr + 0, tag | (k >> 8), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_store(gr + 1, tag | ((k & 0xFFull) << 32) | ib, __ATOMIC_RELAXED,
                                __HIP_MEMORY_SCOPE_AGENT);
+            if constexpr (GUARD) {   // this block's minimum of step t and its row (after the record: off its path)
+                gsc->blk_v[t & 1] = vb;
+                gsc->blk_i[t & 1] = ib;
+            }
         }
     } else if (threadIdx.x < 64) {
         // replicated records: wave 0 combines (every lane the same values from LDS) and lane r
@@ -366,14 +370,7 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
         uint64_t k;
         uint32_t ib;
         combine_waves<NT>(sc, k, ib);
-        if (threadIdx.x == 0) {
-            const double vb = key_value(k);
-            sc->vblk = vb;
-            if constexpr (GUARD) {   // this block's minimum of step t and its row
-                gsc->blk_v[t & 1] = vb;
-                gsc->blk_i[t & 1] = ib;
-            }
-        }
+        if (threadIdx.x == 0) sc->vblk = key_value(k);
         if ((int)threadIdx.x < a.nrep) {
             const uint64_t tag = step_tag(t);
             const uint64_t g0 = tag | (k >> 8), g1 = tag | ((k & 0xFFull) << 32) | ib;
@@ -384,6 +381,12 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
             __builtin_amdgcn_raw_buffer_store_b128(u32x4{(unsigned)g0, (unsigned)(g0 >> 32), (unsigned)g1,
                                                          (unsigned)(g1 >> 32)},
                                                    rsrc, (int)off, 0, 16 /* sc1 */);
+        }
+        if constexpr (GUARD) {   // this block's minimum of step t and its row (after the record: off its path)
+            if (threadIdx.x == 0) {
+                gsc->blk_v[t & 1] = key_value(k);
+                gsc->blk_i[t & 1] = ib;
+            }
         }
     }
 }
@@ -398,6 +401,10 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 // quantise the step: 1.3 us made n = 2.5e5 3.9 us per step).
 #ifndef ST_POLL_SYNC
 #define ST_POLL_SYNC 45
+#endif
+// near-tie guard layout experiment (measurement builds only; the default is the product's)
+#ifndef ST_GUARD_RW0
+#define ST_GUARD_RW0 2
 #endif
 #ifndef ST_POLL_SYNC_FIRST
 #define ST_POLL_SYNC_FIRST 1
@@ -504,9 +511,22 @@ __device__ __forceinline__ double finish_mask(const PersistArgs& a, double o, ui
 // (stein_ref.c tie_init / tie_step, the same operations).  Step 0 first reads the problem's bounds,
 // which every block merged before publishing step 0 (so this block's sweep of step 0 saw them all), or
 // the host wrote before the launch (multi-rank: all n rows)
+// the winner's score row and weight of step t for the recurrence, from the read-only inputs
+template <int D, bool GF>
+struct WinnerG {
+    double g[D], w;
+    __device__ __forceinline__ void load(const PersistArgs& a, const GuardScratch* sc, int64_t t) {
+        const uint32_t gi = sc->win_i[t & 1];
+        const int64_t gr = (int64_t)gi < a.n ? (int64_t)gi : 0;   // a completed pick's row is always < n
+#pragma unroll
+        for (int k = 0; k < D; ++k) g[k] = a.g[(int64_t)k * a.ld + gr];
+        w = GF ? a.w[gr] : 1.0;
+    }
+};
+
 template <int D, bool GF>
 __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc, int64_t t, int64_t r0, int64_t r1,
-                                          int nwaves) {
+                                          int nwaves, const WinnerG<D, GF>& wg) {
     const int par = (int)(t & 1);
     double* ts = sc->tg;   // c1, wmax, Dmax, Q, E, thr
     if (t == 0) {   // stein_ref.c tie_init
@@ -546,15 +566,12 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
         __hip_atomic_fetch_max(a.tie, ~(unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const double Q = ts[3] + v;
-    // the winner's g (and w) from the read-only inputs: Scratch::row may already hold the next step's
-    // winner (this check runs one step late, off the critical path, and the next pick does not wait)
-    double gj[D];
+    // the winner's g row and weight, loaded by the caller at the start of its chain (WinnerG): the loads fly
+    // while it reduces the rescans (Scratch::row may already hold the next step's winner)
+    double gj2 = wg.g[0] * wg.g[0];
 #pragma unroll
-    for (int k = 0; k < D; ++k) gj[k] = a.g[(int64_t)k * a.ld + gr];
-    double gj2 = gj[0] * gj[0];
-#pragma unroll
-    for (int k = 1; k < D; ++k) gj2 = gj2 + gj[k] * gj[k];
-    const double wj = GF ? a.w[gr] : 1.0;
+    for (int k = 1; k < D; ++k) gj2 = gj2 + wg.g[k] * wg.g[k];
+    const double wj = GF ? wg.w : 1.0;
     const double scale = (ts[0] + gj2) * (ts[1] * wj);
     const double E = ts[4] + (16.0 * scale + (2.0 * ts[2] + __builtin_fmax(Q, 0.0)));
     ts[3] = Q;
@@ -571,6 +588,8 @@ __device__ __forceinline__ void tie_check_lanes(const PersistArgs& a, GuardScrat
                                                 int64_t t, int64_t r0, int64_t r1) {
     static_assert(NT <= 256, "GuardLanes holds 256 threads");
     const int par = (int)(t & 1);
+    WinnerG<D, GF> wg;   // issued first: lands while the lanes reduce
+    if ((threadIdx.x & 63) == 0) wg.load(a, sc, t);
     const uint32_t gi = sc->win_i[par];
     const double vmin = sc->blk_v[par];
     if (((int64_t)gi >= r0 && (int64_t)gi < r1) || vmin == sc->win_v[par]) {   // block-uniform
@@ -592,7 +611,7 @@ __device__ __forceinline__ void tie_check_lanes(const PersistArgs& a, GuardScrat
         o = wave_min_f64(o);
         if (lane == 0) sc->rs_o[par][0] = o;
     }
-    if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, t, r0, r1, 1);
+    if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, t, r0, r1, 1, wg);
 }
 
 // wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
@@ -1105,6 +1124,48 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         }
     }
 
+    // near-tie guard: the block's rows that repeat their predecessor row bit for bit (x, g, w) -- a rejected
+    // MCMC proposal.  Such a row has its run's first row's sum at every step, so a tie it shows with the
+    // block's minimum is either with a duplicate of that minimum or a repeat of a tie its run's first row
+    // already counts: the rescans skip it (no duplicate test).  Register rows: bit q of rrep; LDS rows: bit e
+    // of GuardScratch::lrep; streamed rows are tested when they tie (rescan_rest)
+    uint32_t rrep = 0;
+    if constexpr (guard) {
+#pragma unroll
+        for (int q = 0; q < RT; ++q) {
+            const int64_t row = r0 + (int64_t)q * kPBlock + tid;
+            if (row < r1 && row > 0) {
+                bool same = true;
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    same &= same_bits(a.x[k * ld + row - 1], xr[q][k]);
+                    same &= same_bits(a.g[k * ld + row - 1], gr[q][k]);
+                }
+                if constexpr (GF) same &= same_bits(a.w[row - 1], wr[q]);
+                rrep |= same ? 1u << q : 0u;
+            }
+        }
+        for (int e = tid; e < RL; e += kPBlock) {   // RL: whole 64-row chunks, so whole waves
+            const int64_t row = lds_base + e;
+            bool same = false;
+            if (row < r1 && row > 0) {
+                same = true;
+#pragma unroll
+                for (int k = 0; k < D; ++k) {
+                    same &= same_bits(a.x[k * ld + row - 1], lrow(e)[fX + k * 64]);
+                    same &= same_bits(a.g[k * ld + row - 1], lrow(e)[fG + k * 64]);
+                }
+                if constexpr (GF) same &= same_bits(a.w[row - 1], lrow(e)[fW]);
+            }
+            const uint64_t bal = __ballot(same);
+            if ((tid & 63) == 0) {
+                gsc->lrep[(e >> 5)] = (uint32_t)bal;
+                gsc->lrep[(e >> 5) + 1] = (uint32_t)(bal >> 32);
+            }
+        }
+        // (visible to the rescans: they run after publish(0)'s barrier)
+    }
+
     // ---- step 0: diagonal --------------------------------------------------------------------
     // running best of this thread: starts at its first row (register row 0, which precedes all its
     // other rows); an out-of-range row contributes +inf with its (>= n) index and never wins
@@ -1170,9 +1231,14 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
 #pragma unroll
         for (int q = 0; q < RT; ++q) {
             o = __builtin_fmin(o, other_of(ar[q], vmin));
-            msk |= ((ar[q] == vmin) & fin & (row0 + (uint32_t)(q * kPBlock) != ibk)) ? 1u << q : 0u;
+            msk |= ((ar[q] == vmin) & fin & (row0 + (uint32_t)(q * kPBlock) != ibk) & !((rrep >> q) & 1u)) ? 1u << q
+                                                                                                      : 0u;
         }
     };
+    // the LDS and streamed rows' rescan is dealt over waves kRW0 .. kNW - 1: with three or more waves wave 1
+    // keeps only its register rows, so its chain after the publish -- reduce_w0 / tie_check, then its rows --
+    // issues no global load unless a tie needs the duplicate test
+    constexpr int kRW0 = kNW >= 3 ? ST_GUARD_RW0 : 1;
     auto rescan_rest = [&](int64_t tt) {   // waves 1 .. kNW - 1, right after publish(tt)
         // the block's minimum and its row, combined from the wave minima publish(tt) left in Scratch (wave 0
         // writes blk_v / blk_i only after publish's barrier)
@@ -1180,28 +1246,70 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         uint32_t ibk;
         combine_waves<NT>(sc, kmin, ibk);
         const double vmin = key_value(kmin);
+        const bool fin = vmin < INFINITY;
         double o = INFINITY;
-        uint32_t msk = 0;
-        bool tie = false;   // an LDS or streamed row tied with vmin
-        rescan_regs(vmin, ibk, o, msk);
+        uint32_t msk = 0, smsk = 0;   // tied register rows; tied streamed rows by this thread's visit number
+        bool tie = false;             // a tied LDS row, or a tied streamed row past visit 31
+        const int rt0 = tid - 64 * kRW0, rstep = kPBlock - 64 * kRW0;
         if constexpr (!kWide) {
-            for (int e = tid - 64; e < RL; e += kPBlock - 64) {
-                const int64_t row = lds_base + e;
-                const double av = lrow(e)[fA];
-                if (row < r1) {
+            if (wid >= kRW0) {
+                int j = 0;
+                for (int64_t row = str_base + rt0; row < r1; row += rstep, ++j) {
+                    const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
                     o = __builtin_fmin(o, other_of(av, vmin));
-                    tie |= av == vmin && (uint32_t)row != ibk;
+                    const bool tj = av == vmin && fin && (uint32_t)row != ibk;
+                    if (j < 32) smsk |= tj ? 1u << j : 0u;
+                    else tie |= tj;
+                }
+                for (int e = rt0; e < RL; e += rstep) {
+                    const double av = lrow(e)[fA];
+                    if (lds_base + e < r1) {
+                        o = __builtin_fmin(o, other_of(av, vmin));
+                        tie |= av == vmin && fin && (uint32_t)(lds_base + e) != ibk &&
+                               !((gsc->lrep[e >> 5] >> (e & 31)) & 1u);
+                    }
                 }
             }
-            for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64) {
-                const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
-                o = __builtin_fmin(o, other_of(av, vmin));
-                tie |= av == vmin && (uint32_t)row != ibk;
-            }
         }
-        if (__any(msk != 0 || tie)) {   // rows tied with the block's minimum: duplicates of row ibk?
+        rescan_regs(vmin, ibk, o, msk);
+        if (__any(msk != 0 || smsk != 0 || tie)) {   // rows tied with the block's minimum: duplicates of row ibk?
             RowBits<D, GF> b;
             b.load(a, (int64_t)ibk < a.n ? (int64_t)ibk : 0);
+            if constexpr (!kWide) {
+                if (wid >= kRW0) {
+                    int j = 0;
+                    for (int64_t row = str_base + rt0; row < r1; row += rstep, ++j) {
+                        bool tj;
+                        if (j < 32) {
+                            tj = (smsk >> j) & 1u;
+                        } else {
+                            const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
+                            tj = av == vmin && fin && (uint32_t)row != ibk;
+                        }
+                        if (tj) {   // (a repeat of its predecessor row counts nothing new: see rrep)
+                            RowBits<D, GF> r, p;
+                            r.load(a, row);
+                            p.load(a, row > 0 ? row - 1 : row);
+                            if (!(row > 0 && rows_equal(r, p)) && !rows_equal(r, b)) o = __builtin_fmin(o, vmin);
+                        }
+                    }
+                    for (int e = rt0; e < RL; e += rstep) {
+                        const int64_t row = lds_base + e;
+                        const double* rp = lrow(e);
+                        if (row < r1 && rp[fA] == vmin && fin && (uint32_t)row != ibk &&
+                            !((gsc->lrep[e >> 5] >> (e & 31)) & 1u)) {
+                            bool same = true;
+#pragma unroll
+                            for (int k = 0; k < D; ++k) {
+                                same &= same_bits(rp[fX + k * 64], b.v[k]);
+                                same &= same_bits(rp[fG + k * 64], b.v[D + k]);
+                            }
+                            if constexpr (GF) same &= same_bits(rp[fW], b.v[2 * D]);
+                            if (!same) o = __builtin_fmin(o, vmin);
+                        }
+                    }
+                }
+            }
 #pragma unroll
             for (int q = 0; q < RT; ++q) {
                 if ((msk >> q) & 1u) {
@@ -1215,30 +1323,6 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                     if (!same) o = __builtin_fmin(o, vmin);
                 }
             }
-            if constexpr (!kWide) {
-                for (int e = tid - 64; e < RL; e += kPBlock - 64) {
-                    const int64_t row = lds_base + e;
-                    const double* rp = lrow(e);
-                    if (row < r1 && rp[fA] == vmin && (uint32_t)row != ibk) {
-                        bool same = true;
-#pragma unroll
-                        for (int k = 0; k < D; ++k) {
-                            same &= same_bits(rp[fX + k * 64], b.v[k]);
-                            same &= same_bits(rp[fG + k * 64], b.v[D + k]);
-                        }
-                        if constexpr (GF) same &= same_bits(rp[fW], b.v[2 * D]);
-                        if (!same) o = __builtin_fmin(o, vmin);
-                    }
-                }
-                for (int64_t row = str_base + tid - 64; row < r1; row += kPBlock - 64) {
-                    const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
-                    if (av == vmin && (uint32_t)row != ibk) {
-                        RowBits<D, GF> r;
-                        r.load(a, row);
-                        if (!rows_equal(r, b)) o = __builtin_fmin(o, vmin);
-                    }
-                }
-            }
         }
         const int par = (int)(tt & 1);
         if constexpr (kLanes) {   // per thread, reduced only where tie_check needs it (tie_check_lanes)
@@ -1248,6 +1332,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             o = wave_min_f64(o);
             if ((tid & 63) == 0) gsc->rs_o[par][wid] = o;
         }
+        ST_STAMP_WAVE(a, tt, 24);   // diagnostic build: this wave's rescan of step tt done (phase 24 + wave)
     };
     // wave 0's own rescan leaves its lanes' "other" and tied-row masks in LDS; the duplicate test and the
     // reduction follow after the next publish (wave 1: reduce_w0; the 256-thread kernels: tie_check_lanes)
@@ -1590,8 +1675,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                     if constexpr (kLanes) {
                         tie_check_lanes<D, GF, NT>(a, gsc, gl, t - 1, r0, r1);
                     } else {
+                        WinnerG<D, GF> wg;   // issued first: lands while wave 0's lanes are reduced
+                        if (tid == 64) wg.load(a, gsc, t - 1);
                         reduce_w0(t - 1);   // wave 0's lanes of step t - 1
-                        if (tid == 64) tie_check<D, GF>(a, gsc, t - 1, r0, r1, kNW);
+                        if (tid == 64) tie_check<D, GF>(a, gsc, t - 1, r0, r1, kNW, wg);
                     }
                 }
                 rescan_rest(t);
@@ -1617,7 +1704,11 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             else reduce_w0(a.m - 1);
         }
         if (tid == 64 && done == a.m + 1) {
-            if constexpr (!kLanes) tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW);
+            if constexpr (!kLanes) {
+                WinnerG<D, GF> wg;
+                wg.load(a, gsc, a.m - 1);
+                tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW, wg);
+            }
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)
                 double* st_out = const_cast<double*>(a.tie_bounds) + 2;
                 st_out[0] = gsc->tg[3];

@@ -57,13 +57,14 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * Kernel-variant tuning (process-wide, host side; for measurement sweeps -- defaults are the
  * measured best on MI355X): key 0 = grid cap (blocks, 1..1024), key 1 = candidates per lane
  * (1, 2, 4; d = 2 and 4 kernels; -1 = automatic), key 2 = register prefetch of the next tile
- * (0/1; -1 = automatic), key 3 = persistent kernel register rows per thread (4, 8, 16; 1, 2 on
- * 256-thread blocks whose rows they hold; -1 = automatic: 1 / 2 for blocks of at most 256 / 512 rows,
- * else the fewest of 16 / 8 / 4 without empty rows; 0 = disable the persistent kernel), key 4 = persistent kernel threads per
+ * (0/1; -1 = automatic), key 3 = persistent kernel register rows per thread (4, 8 on 512-thread blocks;
+ * 1, 2, 4 on 256-thread blocks; -1 = automatic: 1 / 2 for blocks of at most 256 / 512 rows, 4 on other
+ * 256-thread blocks, 8 on 512-thread blocks unless that leaves slots empty, then 4; 0 = disable the
+ * persistent kernel; round 6 pruned the plans that won nothing), key 4 = persistent kernel threads per
  * block (256, 512; -1 = automatic: 512 with dynamic chunks above 1280 rows per block), key 5 = persistent kernel grid cap (blocks per device,
  * 1..256; -1 = one per CU), key 6 = grid cap of the d > 8 step kernel (1..1024), key 7 = proxy
  * kernel (0 = automatic: matrix cores for 16 < d <= 64; 1 = always the VALU kernel), key 8 =
- * persistent kernel blocks per CU (1, 2; -1 = automatic = 1), key 9 = persistent kernel
+ * persistent kernel blocks per CU (1 / -1 only: the two-block plans were pruned in round 6), key 9 = persistent kernel
  * record pitch in bytes (power of two, 16..4096; -1 = automatic = 256 with one replica, 16 with
  * several, narrowed to what the workspace holds), key 10 = persistent kernel record replicas
  * (power of two, 1..32: every block stores its per-step record into each replica and block b
@@ -72,9 +73,8 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * ulps from NumPy's evaluation, for every pair whose two rows and l, tr lie in [2^-60, 2^60];
  * 0 = exact: NumPy's evaluation order rounding for rounding; other pairs are always exact -- see
  * oracle/stein_ref.c and DESIGN.md §3; all ranks of a sharded run must use the same value), key 12 =
- * register rows per thread of the one-device compact-only persistent kernel (4, 6, 8 .. 10; 0 = do
- * not use it; -1 = automatic: from 8 x 512 rows per block 9 (8 under the near-tie guard), or 10 when more than 2048 rows per block
- * would still be streamed; below that 4 up to 2 560 rows per block, else 6), key 13 = energy-distance kernel variant (0 / -1 = automatic = 1:
+ * register rows per thread of the one-device compact-only persistent kernel, used from 8 x 512 rows per
+ * block (8, 9; 0 = do not use it; -1 = automatic: 9, or 8 under the near-tie guard), key 13 = energy-distance kernel variant (0 / -1 = automatic = 1:
  * one partial sum per thread, 4 blocks per CU; 2..5: more partial sums or 8 blocks per CU; 6: the
  * round-2 zero-distance select -- measured alternatives; same distances, sums within
  * rounding), key 14 = energy-distance work units: grid blocks (256 columns x one B chunk) that

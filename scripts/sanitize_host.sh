@@ -27,7 +27,7 @@ if [[ $WHAT == all || $WHAT == abi ]]; then
   $HIPCC --offload-arch=gfx950 -O1 -g -std=c++17 -ffp-contract=off -Xarch_host -fsanitize=address \
     -Xarch_host -fsanitize=undefined -Xarch_host -fno-sanitize-recover=all -Xarch_host -fno-omit-frame-pointer \
     -o $OUT/abi_asan tools/sanitize/abi_invalid_check.cpp $CS/capi.hip $CS/dedup.hip $CS/precon.hip $CS/greedy.hip \
-    $CS/persistent.hip $CS/persistent_guard.hip $CS/persistent_small.hip $CS/persistent_cmp.hip $CS/pairwise.hip $CS/proxy.hip $CS/kde.hip \
+    $CS/persistent.hip $CS/persistent_guard.hip $CS/persistent_small.hip $CS/pairwise.hip $CS/proxy.hip $CS/kde.hip \
     $CS/lv.hip $CS/host_prep.cpp $CS/prep_upload.cpp
   $OUT/abi_asan
 fi

@@ -169,8 +169,9 @@ def test_tune_keys_validate_without_gpu(libpath):
     from stein_thinning import _native
     lib = _native.load_library(libpath)
     for key, good, bad in [(10, [1, 2, 16, 32], [0, 3, 64]), (9, [16, 256, 4096], [8, 24, 8192]),
-                           (4, [256, 512], [128, 1024]), (8, [1, 2], [3]), (11, [0, 1], [2, -2]),
-                           (12, [0, 8, 9, 10], [7, 11]), (13, [0, 1, 2, 5, 6], [7, -2]),
+                           (4, [256, 512], [128, 1024]), (8, [1], [2, 3]), (11, [0, 1], [2, -2]),
+                           (12, [0, 8, 9], [4, 6, 7, 10, 11]), (13, [0, 1, 2, 5, 6], [7, -2]),
+                           (3, [0, 1, 2, 4, 8, 16], [3, 6, 32]), (22, [0, 1], [2, -2]), (23, [1, 64, 512], [0, 513]),
                            (17, [0, 1], [2, -2]), (18, [1, 2, 3], [0, 4]), (19, [0, 1], [2, -2])]:
         for v in good:
             assert lib.st_tune(key, v) == 0, (key, v)

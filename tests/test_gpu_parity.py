@@ -161,7 +161,7 @@ def test_running_sums_bit_exact_vs_c_model(d, gf, mode):
 
 @pytest.mark.parametrize('tune', [
     ('persistent: registers + LDS + streamed rows', 4, 1_000_003, 4),
-    ('persistent: registers only', 16, 30_011, 4),
+    ('persistent: registers only', 4, 30_011, 4),
     ('persistent: d=2 gradient-free', -1, 200_003, 2),
     ('launch-per-step path', 0, 300_007, 4),
 ])
@@ -190,22 +190,18 @@ def test_persistent_and_fallback_bit_exact(tune):
 
 
 @pytest.mark.parametrize('knobs', [
-    ('two blocks per CU, 8 register rows', {8: 2}),
-    ('two blocks per CU, 4 register rows', {8: 2, 3: 4}),
     ('512-thread blocks, 8 register rows', {4: 512, 3: 8}),
-    ('512-thread blocks, 6 register rows', {4: 512, 3: 6}),
     ('512-thread blocks, 4 register rows', {4: 512, 3: 4}),
     ('256-thread blocks (one wave per SIMD), LDS and streamed rows', {4: 256}),
     ('512-thread blocks, packed 16-B records', {4: 512, 9: 16}),
     ('one record array, 256-B pitch (no replicas)', {10: 1}),
     ('4 record replicas', {10: 4}),
     ('32 record replicas, 64-B pitch', {10: 32, 9: 64}),
-    ('two blocks per CU, 32 record replicas (512 records per step)', {8: 2, 10: 32}),
 ])
 @pytest.mark.parametrize('d,gf', [(4, False), (2, True)])
 def test_persistent_two_wave_variants_bit_exact(knobs, d, gf):
-    """The optional two-waves-per-SIMD persistent variants (st_tune keys 3, 4, 8) and record
-    layouts (keys 9, 10) against the C model: identical indices, bit-identical running sums."""
+    """The persistent plans forced through st_tune (keys 3, 4: threads per block and register rows) and the
+    record layouts (keys 9, 10) against the C model: identical indices, bit-identical running sums."""
     from stein_thinning import _native
     n, m = 700_001, 20
     x, g = _rw_chain(n, d, seed=11 + d)

@@ -218,7 +218,7 @@ int main(int argc, char** argv) {
     }
     // whole-run st_greedy: persistent kernel (register rows per thread rt; 0 = launch per step)
     struct V { int rt, nt; };
-    for (V cfg : {V{8, 512}, V{6, 512}, V{4, 512}, V{16, 256}, V{0, 256}}) {
+    for (V cfg : {V{8, 512}, V{4, 512}, V{4, 256}, V{0, 256}}) {
         const int rt = cfg.rt;
         st_tune(3, rt);
         st_tune(4, cfg.nt);
@@ -239,7 +239,7 @@ int main(int argc, char** argv) {
     st_tune(4, -1);
 #ifdef ST_PERSIST_STAMPS
     {   // phase breakdown of persistent steps 20..51 (s_memrealtime, 10 ns ticks)
-        const int SP = 32, PH = 24, GMAX = 512;
+        const int SP = 32, PH = 32, GMAX = 512;
         if (getenv("PROBE_BPC")) st_tune(8, atoi(getenv("PROBE_BPC")));
         if (getenv("PROBE_NT")) st_tune(4, atoi(getenv("PROBE_NT")));
         if (getenv("PROBE_RT")) st_tune(3, atoi(getenv("PROBE_RT")));
@@ -330,6 +330,25 @@ int main(int argc, char** argv) {
             printf("publish split (us): wave0 minloc %.2f  waves' compute-end spread %.2f (wave0 -> last %.2f)  "
                    "last wave end -> barrier passed %.2f  barrier -> record stored %.2f\n",
                    ml / cntp / 100, spread / cntp / 100, w0_to_last / cntp / 100, bar / cntp / 100, st / cntp / 100);
+        }
+        {   // near-tie guard (diagnostic): the latest wave's rescan of step st (phase 24 + w) against the block's
+            // sweep of that step done (phase 1 of row st + 1): > 0 = the rescan holds the next step's barrier
+            double late = 0, lat_max = 0;
+            int cntr = 0;
+            const int NW = getenv("PROBE_NT") && atoi(getenv("PROBE_NT")) == 256 ? 4 : 8;
+            for (int stp = 1; stp + 1 < SP; ++stp)
+                for (int b = 0; b < G; ++b) {
+                    const uint64_t* q = &h[((size_t)b * SP + stp) * PH];
+                    const uint64_t* nx = &h[((size_t)b * SP + stp + 1) * PH];
+                    uint64_t hi = 0;
+                    for (int w = 1; w < NW; ++w) hi = std::max<uint64_t>(hi, q[24 + w]);
+                    if (hi == 0) continue;
+                    const double d = ((double)hi - (double)nx[1]) / 100;
+                    late += d;
+                    lat_max = std::max(lat_max, d);
+                    ++cntr;
+                }
+            if (cntr) printf("guard rescan end - sweep done: %.2f us on average, %.2f max\n", late / cntr, lat_max);
         }
         printf("compute split (us): register rows %.2f  LDS rows %.2f  streamed rows %.2f\n",
                acc[7] / cnt / 100, ph_lds / cnt / 100, (acc[0] - acc[7] - ph_lds) / cnt / 100);
