@@ -175,6 +175,8 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
         } else {
             return hipErrorNotSupported;
         }
+    } else if constexpr (!GEN && RT < 8) {   // the mid-size compact-only plan is a guarded plan only
+        return hipErrorNotSupported;
     } else if (b) {
         if constexpr (BPC == 1 && D <= kMaxCtDim) {
             if (!arith_compact()) return hipErrorNotSupported;
@@ -215,11 +217,12 @@ static hipError_t launch_p(const PersistArgs& a, int G, size_t lds, hipStream_t 
     return hipLaunchKernel(fn, dim3(G), dim3(NT), kargs, lds, s);
 }
 
-// compact-only kernels: 512-thread blocks, 8 / 9 register rows per thread
+// compact-only kernels: 512-thread blocks, 8 / 9 register rows per thread (4 under the near-tie guard)
 template <int D, bool GF>
 static hipError_t launch_p_cmp(const PersistArgs& a, int rt, int G, size_t lds, hipStream_t s, bool dry,
                                const BatchArgs* b) {
     if (rt == 9) return launch_p<D, GF, 9, 512, 1, false>(a, G, lds, s, dry, b);
+    if (rt == 4) return launch_p<D, GF, 4, 512, 1, false>(a, G, lds, s, dry, b);
     return launch_p<D, GF, 8, 512, 1, false>(a, G, lds, s, dry, b);
 }
 
@@ -329,6 +332,9 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     if (rt != 4 && rt != 8 && !(small_ok && (rt == 1 || rt == 2))) rt = rt_max;
     if (rt > rt_max) rt = rt_max;
     if (rt == 8 && (int64_t)rt * nt > R) rt = 4;   // no empty register rows
+    // the near-tie guard's general kernel: 4 register rows (with 8 its guard state spills ~0.7 KB per lane
+    // inside the step loop; it runs where the compact-only kernel does not -- a rank of a multi-rank thin)
+    if (rt == 8 && nt == 512 && tie_guard() && arith_compact() && g_persist_rt <= 0 && rt_force <= 0) rt = 4;
     // small shards: the fewest register rows that hold the block's rows (padding rows compute like real
     // ones; 1 / 2 rows per thread at <= 256 / 512 rows per block)
     if (small_ok && g_persist_rt <= 0 && rt_force <= 0 && R <= 2 * 256) rt = R <= 256 ? 1 : 2;
@@ -408,11 +414,17 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     bool use_cmp = false;
     int rt_c = 0;
     size_t lds_c = 0;
-    // (round 5's mid-size compact-only plans -- 4 / 6 register rows from 1 280 rows per block -- gained 1.5 % on
-    // the LV call and nothing on a BASELINE config; pruned in round 6 with the other families below the 3 % bar)
-    if (rs->nranks == 1 && arith_compact() && nt == 512 && !wide && g_persist_cmp != 0 && R >= 8 * 512) {
+    // Mid-size blocks (1 280 .. 4 095 rows): unguarded, the general kernel (round 5's compact-only 4 / 6-row
+    // plans gained 1.5 % on the LV call and were pruned in round 6 with the other families below the 3 % bar);
+    // guarded, the compact-only kernel of 4 register rows -- the guarded general kernel of 4 rows spills, and
+    // the LV call's all-row thin takes 44.6 ms on it against 40.7 ms (profiles/r06_plans_ab.log)
+    const bool mid_guard = guard && !batch && cmp_force <= 0 && R >= 1280 && R < 8 * 512;
+    if (rs->nranks == 1 && arith_compact() && nt == 512 && !wide && g_persist_cmp != 0 &&
+        (R >= 8 * 512 || mid_guard)) {
         if (cmp_force > 0)
             rt_c = cmp_force;   // a batch's common register rows (launch_greedy_persistent_batch)
+        else if (mid_guard)
+            rt_c = 4;
         else
             rt_c = g_persist_cmp > 0 ? g_persist_cmp : 9;
         // guarded: 8 register rows -- the guard's rescans take the registers a ninth row needs (9 rows spill

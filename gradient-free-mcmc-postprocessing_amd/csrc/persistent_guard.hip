@@ -23,7 +23,11 @@ template <int D, bool GF>
 const void* pick(int rt, int nt, int bpc, bool gen, bool batch) {
     if (bpc != 1) return nullptr;
     if (!gen) {   // compact-only kernels: 512 threads, 8 register rows (9 only when st_tune key 12 asks: persistent.hip)
-        if (nt != 512 || rt < 8 || rt > 9) return nullptr;
+        if (nt != 512) return nullptr;
+        // 4 register rows: the guarded mid-size plan (1 280 .. 4 095 rows per block, one thin at a time) --
+        // the general kernel of 4 rows spills under the guard (28 B of scratch at d = 4), this one does not
+        if (rt == 4) return batch ? nullptr : kernel<D, GF, 4, 512, 1, false>(false);
+        if (rt < 8 || rt > 9) return nullptr;
         return rt == 9 ? kernel<D, GF, 9, 512, 1, false>(batch) : kernel<D, GF, 8, 512, 1, false>(batch);
     }
     if (nt == 512) {

@@ -25,7 +25,7 @@ for key in "${KEYS[@]}"; do
     out=gpurun_out/pmc/${key}_${ctr}
     echo "=== $key $ctr ($(date +%T))"
     timeout -s KILL 240 rocprofv3 --pmc $ctr --output-format csv -d $out -o pmc -- \
-      python3 bench.py ${ARGS[$key]} --steps 1 --warmup 0 --no-cpu-baseline > $out.log 2>&1
+      python3 bench.py ${ARGS[$key]} --steps ${PMC_STEPS:-1} --warmup ${PMC_WARMUP:-0} --no-cpu-baseline > $out.log 2>&1
     rc=$?
     echo "rc=$rc"; tail -n 2 $out.log
     [[ $rc == 0 ]] || exit $rc

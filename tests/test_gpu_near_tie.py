@@ -226,6 +226,24 @@ def test_dropin_equals_numpy_on_near_ties_at_scale(n):
     assert step == np.flatnonzero(flagged)[0]
 
 
+@pytest.mark.parametrize('shape', ['exp', 'log'])
+def test_lv_call_all_rows_guarded_mid_size_plan(shape):
+    """The LV call's 5e5 rows without dedup (1 954 rows per block): the guarded mid-size plan (the
+    compact-only kernel of 4 register rows, persistent.hip mid_guard) -- indices, flag and final guard state
+    equal the bit model over 300 steps."""
+    from bench import lv_call_shape
+    sample, grads = lv_call_shape(500_000, 12350, shape)
+    integrand = st._make_stein_integrand(sample, grads, preconditioner='med')
+    idx, step, state = _compact_run(integrand.device_problem(), 300)
+    midx, _, _, _, flagged, wv = oc.greedy_ties(integrand.sample, integrand.gradient, None, integrand.linv_scale,
+                                                integrand.linv_trace, 300, winner_sums=True)
+    np.testing.assert_array_equal(idx, midx)
+    assert step == (np.flatnonzero(flagged)[0] if flagged.any() else -1)
+    thr_all, Q, E = model_thresholds(integrand.gradient, None, integrand.linv_scale, integrand.linv_trace, midx, wv)
+    g2, w2 = oc.tie_bounds(integrand.gradient, None)
+    np.testing.assert_array_equal(state, [g2, w2, Q, E, thr_all[-1]])
+
+
 @pytest.mark.parametrize('n', [60, 300, 700, 5000])
 def test_kernel_state_on_few_blocks_long_runs(n):
     """One to twenty blocks and up to 300 steps: the exchange is at its fastest, so the next pick lands

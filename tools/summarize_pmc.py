@@ -35,10 +35,14 @@ def main():
         vals = [v for (k, c), v in agg.items() if c == counter and args.kernel in k and args.exclude not in k]
         names = [k for (k, c) in agg if c == counter and args.kernel in k and args.exclude not in k]
         assert len(vals) == 1, names
-        return names[0], sum(vals[0]) / len(vals[0]), len(vals[0])
-    kname, fetch_kib, nf = pick(f, 'FETCH_SIZE')
-    _, write_kib, nw = pick(w, 'WRITE_SIZE')
+        return names[0], sum(vals[0]) / len(vals[0]), len(vals[0]), vals[0]
+    kname, fetch_kib, nf, fl = pick(f, 'FETCH_SIZE')
+    _, write_kib, nw, wl = pick(w, 'WRITE_SIZE')
     rec = {'kernel': kname, 'launches_fetch': nf, 'launches_write': nw,
+           # each dispatch separately (MB, corrected): the persistent kernels' reads are mostly the exchange's
+           # polls of remote records and vary with how many polls each step takes
+           'read_MB_per_dispatch': [round(2 * v / 1024, 1) for v in fl],
+           'write_MB_per_dispatch': [round(v / 1024, 1) for v in wl],
            'note': ('8-B-per-lane loads (dwordx2) are outside the guide\'s calibration; the same 128-B-request '
                     'x2 correction is applied') if 'persistent' in kname else '',
            'FETCH_SIZE_KiB_per_launch': fetch_kib, 'WRITE_SIZE_KiB_per_launch': write_kib,
