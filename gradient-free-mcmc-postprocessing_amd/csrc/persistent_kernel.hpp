@@ -73,8 +73,6 @@ struct GuardScratch {
     uint32_t win_i[2], blk_i[2];
     double win_v[2], blk_v[2];
     double tg[6];         // recurrence state (stein_ref.c tie_state): c1, wmax, Dmax, Q, E, thr
-    // 512-thread kernels: |g_j|^2 and w_j of step t's winner, from the winner row of step t + 1's sweep
-    double wg2[2], wgw[2];
     double bnd[kMaxPWaves][2];   // per wave: max_i |g_i|^2, max_i w_i^2 over its rows (staging)
     // 512-thread kernels: wave 0's per-lane rescan of its register rows (step t - 1, written at the start
     // of step t) -- the lane's "other" and the mask of its register rows whose sum equals the block's
@@ -408,10 +406,6 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 #ifndef ST_GUARD_RW0
 #define ST_GUARD_RW0 2
 #endif
-// the rescan's streamed / LDS row loops: loads in flight per wave before the first is used
-#ifndef ST_GUARD_UNROLL
-#define ST_GUARD_UNROLL 1
-#endif
 #ifndef ST_POLL_SYNC_FIRST
 #define ST_POLL_SYNC_FIRST 1
 #endif
@@ -441,14 +435,6 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 // the same check against the global winner (each rank flags its own rows; the host combines the ranks'
 // words with one all-reduce after the run) over bounds the host computed from all n rows beforehand.
 
-// a wave-uniform double into SGPRs (the guard's rows compared against ibk keep no VGPRs live)
-__device__ __forceinline__ double uniform_f64(double v) {
-    const uint64_t b = (uint64_t)__double_as_longlong(v);
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
-    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
-}
-
 // the row (x, g[, w]) of row r from the read-only inputs
 template <int D, bool GF>
 struct RowBits {
@@ -461,47 +447,10 @@ struct RowBits {
         }
         if constexpr (GF) v[2 * D] = a.w[r];
     }
-    // the same row for every lane of the wave (r wave-uniform; every lane active): held in SGPRs
-    __device__ __forceinline__ void load_uniform(const PersistArgs& a, int64_t r) {
-        r = (int64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)r);   // rows < 2^31
-        load(a, r);
-#pragma unroll
-        for (int k = 0; k < 2 * D + (GF ? 1 : 0); ++k) v[k] = uniform_f64(v[k]);
-    }
 };
 
 __device__ __forceinline__ bool same_bits(double p, double q) {
     return __double_as_longlong(p) == __double_as_longlong(q);
-}
-
-
-// row r (per lane) against row b (wave-uniform): bitwise equal?  One field at a time, so that only the
-// three values of one field are live (the duplicate tests run beside the register rows)
-template <int D, bool GF>
-__device__ __forceinline__ bool row_equals_at(const PersistArgs& a, int64_t r, int64_t b) {
-    bool eq = true;
-#pragma unroll 1
-    for (int f = 0; f < 2 * D + (GF ? 1 : 0); ++f) {
-        const double* col = f < D ? a.x + (int64_t)f * a.ld : (f < 2 * D ? a.g + (int64_t)(f - D) * a.ld : a.w);
-        eq &= same_bits(col[r], col[b]);
-    }
-    return eq;
-}
-
-// the streamed-row test of the rescan: row r differs from both its predecessor (a repeat counts nothing
-// new) and row b
-template <int D, bool GF>
-__device__ __forceinline__ bool new_tie_at(const PersistArgs& a, int64_t r, int64_t b) {
-    bool eqp = r > 0, eqb = true;
-    const int64_t p = r > 0 ? r - 1 : r;
-#pragma unroll 1
-    for (int f = 0; f < 2 * D + (GF ? 1 : 0); ++f) {
-        const double* col = f < D ? a.x + (int64_t)f * a.ld : (f < 2 * D ? a.g + (int64_t)(f - D) * a.ld : a.w);
-        const double rv = col[r];
-        eqp &= same_bits(rv, col[p]);
-        eqb &= same_bits(rv, col[b]);
-    }
-    return !eqp && !eqb;
 }
 
 template <int D, bool GF>
@@ -543,16 +492,17 @@ __device__ __forceinline__ double wave_min_f64(double m) {
 }
 
 // The duplicate test of register rows recorded as a mask (wave 0's rows): thread `owner`'s register rows
-// q set in `msk` (rows r0 + q * NT + owner, sum == vmin) are compared with row bi (ibk, clamped to a row)
-// through global loads; a row that differs contributes vmin.  Per lane; the caller keeps it behind a
-// wave-uniform branch.
+// q set in `msk` (rows r0 + q * NT + owner, sum == vmin) are compared with row ibk through global loads; a
+// row that differs contributes vmin.  Per lane; the caller keeps it behind a wave-uniform branch.
 template <int D, bool GF, int NT>
 __device__ __forceinline__ double finish_mask(const PersistArgs& a, double o, uint32_t msk, int owner, int64_t r0,
-                                              double vmin, int64_t bi) {
+                                              double vmin, const RowBits<D, GF>& b) {
     while (msk) {
         const int q = __builtin_ctz(msk);
         msk &= msk - 1;
-        if (!row_equals_at<D, GF>(a, r0 + (int64_t)q * NT + owner, bi)) o = __builtin_fmin(o, vmin);
+        RowBits<D, GF> r;
+        r.load(a, r0 + (int64_t)q * NT + owner);
+        if (!rows_equal(r, b)) o = __builtin_fmin(o, vmin);
     }
     return o;
 }
@@ -561,15 +511,6 @@ __device__ __forceinline__ double finish_mask(const PersistArgs& a, double o, ui
 // (stein_ref.c tie_init / tie_step, the same operations).  Step 0 first reads the problem's bounds,
 // which every block merged before publishing step 0 (so this block's sweep of step 0 saw them all), or
 // the host wrote before the launch (multi-rank: all n rows)
-// |g_j|^2 of the recurrence (stein_ref.c tie_step: the same order of operations)
-template <int D>
-__device__ __forceinline__ double winner_g2(const double* g) {
-    double gj2 = g[0] * g[0];
-#pragma unroll
-    for (int k = 1; k < D; ++k) gj2 = gj2 + g[k] * g[k];
-    return gj2;
-}
-
 // the winner's score row and weight of step t for the recurrence, from the read-only inputs
 template <int D, bool GF>
 struct WinnerG {
@@ -581,12 +522,11 @@ struct WinnerG {
         for (int k = 0; k < D; ++k) g[k] = a.g[(int64_t)k * a.ld + gr];
         w = GF ? a.w[gr] : 1.0;
     }
-    __device__ __forceinline__ double g2() const { return winner_g2<D>(g); }
 };
 
 template <int D, bool GF>
 __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc, int64_t t, int64_t r0, int64_t r1,
-                                          int nwaves, double gj2, double wj) {
+                                          int nwaves, const WinnerG<D, GF>& wg) {
     const int par = (int)(t & 1);
     double* ts = sc->tg;   // c1, wmax, Dmax, Q, E, thr
     if (t == 0) {   // stein_ref.c tie_init
@@ -612,7 +552,10 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
     bool rest = (int64_t)gi >= r0 && (int64_t)gi < r1;   // the winner's block: its "other"
     if (!rest && other == v) {   // this block's minimum ties the winner's sum: a duplicate of the winner?
         const uint32_t bi = sc->blk_i[par];
-        rest = row_equals_at<D, GF>(a, gr, (int64_t)bi < a.n ? (int64_t)bi : 0);
+        RowBits<D, GF> p, q;
+        p.load(a, gr);
+        q.load(a, (int64_t)bi < a.n ? (int64_t)bi : 0);
+        rest = rows_equal(p, q);
     }
     if (rest) {
         other = INFINITY;
@@ -623,8 +566,12 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
         __hip_atomic_fetch_max(a.tie, ~(unsigned)t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     const double Q = ts[3] + v;
-    // gj2 / wj: the winner's |g|^2 and weight (512-thread kernels: GuardScratch::wg2 / wgw, from the winner
-    // row the next step's sweep used; else WinnerG, loaded by the caller at the start of its chain)
+    // the winner's g row and weight, loaded by the caller at the start of its chain (WinnerG): the loads fly
+    // while it reduces the rescans (Scratch::row may already hold the next step's winner)
+    double gj2 = wg.g[0] * wg.g[0];
+#pragma unroll
+    for (int k = 1; k < D; ++k) gj2 = gj2 + wg.g[k] * wg.g[k];
+    const double wj = GF ? wg.w : 1.0;
     const double scale = (ts[0] + gj2) * (ts[1] * wj);
     const double E = ts[4] + (16.0 * scale + (2.0 * ts[2] + __builtin_fmax(Q, 0.0)));
     ts[3] = Q;
@@ -656,14 +603,15 @@ __device__ __forceinline__ void tie_check_lanes(const PersistArgs& a, GuardScrat
         }
         if (__any(any != 0)) {
             const uint32_t bi = sc->blk_i[par];
-            const int64_t bc = (int64_t)bi < a.n ? (int64_t)bi : 0;
+            RowBits<D, GF> b;
+            b.load(a, (int64_t)bi < a.n ? (int64_t)bi : 0);
 #pragma unroll
-            for (int k = lane; k < NT; k += 64) o = finish_mask<D, GF, NT>(a, o, gl->m[par][k], k, r0, vmin, bc);
+            for (int k = lane; k < NT; k += 64) o = finish_mask<D, GF, NT>(a, o, gl->m[par][k], k, r0, vmin, b);
         }
         o = wave_min_f64(o);
         if (lane == 0) sc->rs_o[par][0] = o;
     }
-    if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, t, r0, r1, 1, wg.g2(), GF ? wg.w : 1.0);
+    if ((threadIdx.x & 63) == 0) tie_check<D, GF>(a, sc, t, r0, r1, 1, wg);
 }
 
 // wave 0 sweeps the G records of step t until every tag matches (bounded) and reduces them
@@ -1306,7 +1254,6 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         if constexpr (!kWide) {
             if (wid >= kRW0) {
                 int j = 0;
-#pragma unroll ST_GUARD_UNROLL
                 for (int64_t row = str_base + rt0; row < r1; row += rstep, ++j) {
                     const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
                     o = __builtin_fmin(o, other_of(av, vmin));
@@ -1314,7 +1261,6 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                     if (j < 32) smsk |= tj ? 1u << j : 0u;
                     else tie |= tj;
                 }
-#pragma unroll ST_GUARD_UNROLL
                 for (int e = rt0; e < RL; e += rstep) {
                     const double av = lrow(e)[fA];
                     if (lds_base + e < r1) {
@@ -1327,9 +1273,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         }
         rescan_regs(vmin, ibk, o, msk);
         if (__any(msk != 0 || smsk != 0 || tie)) {   // rows tied with the block's minimum: duplicates of row ibk?
-            const int64_t bc = (int64_t)ibk < a.n ? (int64_t)ibk : 0;
-            RowBits<D, GF> b;   // wave-uniform: SGPRs
-            b.load_uniform(a, bc);
+            RowBits<D, GF> b;
+            b.load(a, (int64_t)ibk < a.n ? (int64_t)ibk : 0);
             if constexpr (!kWide) {
                 if (wid >= kRW0) {
                     int j = 0;
@@ -1341,8 +1286,12 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                             const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
                             tj = av == vmin && fin && (uint32_t)row != ibk;
                         }
-                        // (a repeat of its predecessor row counts nothing new: see rrep)
-                        if (tj && new_tie_at<D, GF>(a, row, bc)) o = __builtin_fmin(o, vmin);
+                        if (tj) {   // (a repeat of its predecessor row counts nothing new: see rrep)
+                            RowBits<D, GF> r, p;
+                            r.load(a, row);
+                            p.load(a, row > 0 ? row - 1 : row);
+                            if (!(row > 0 && rows_equal(r, p)) && !rows_equal(r, b)) o = __builtin_fmin(o, vmin);
+                        }
                     }
                     for (int e = rt0; e < RL; e += rstep) {
                         const int64_t row = lds_base + e;
@@ -1408,7 +1357,9 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         const uint32_t msk = gsc->w0_m[lane];
         if (__any(msk != 0)) {
             const uint32_t ibk = gsc->blk_i[par];
-            o = finish_mask<D, GF, NT>(a, o, msk, lane, r0, gsc->blk_v[par], (int64_t)ibk < a.n ? (int64_t)ibk : 0);
+            RowBits<D, GF> b;
+            b.load(a, (int64_t)ibk < a.n ? (int64_t)ibk : 0);
+            o = finish_mask<D, GF, NT>(a, o, msk, lane, r0, gsc->blk_v[par], b);
         }
         o = wave_min_f64(o);
         if (lane == 0) gsc->rs_o[par][0] = o;
@@ -1452,12 +1403,6 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             jok &= rowok;
         }
         const double wj = GF ? uniform(sc->row[2 * D]) : 1.0;
-        if constexpr (guard && !kLanes) {   // step t - 1's winner for its late check (tie_check, after publish(t))
-            if (tid == 64) {
-                gsc->wg2[(t - 1) & 1] = winner_g2<D>(gj);
-                gsc->wgw[(t - 1) & 1] = wj;
-            }
-        }
         // one block-uniform choice per step: range-guarded fast arithmetic or the general one
         auto sweep_rows = [&](auto ar_tag) {
             constexpr int AR = decltype(ar_tag)::value;
@@ -1730,11 +1675,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                     if constexpr (kLanes) {
                         tie_check_lanes<D, GF, NT>(a, gsc, gl, t - 1, r0, r1);
                     } else {
+                        WinnerG<D, GF> wg;   // issued first: lands while wave 0's lanes are reduced
+                        if (tid == 64) wg.load(a, gsc, t - 1);
                         reduce_w0(t - 1);   // wave 0's lanes of step t - 1
-                        if (tid == 64) {
-                            const int wp = (int)((t - 1) & 1);
-                            tie_check<D, GF>(a, gsc, t - 1, r0, r1, kNW, gsc->wg2[wp], gsc->wgw[wp]);
-                        }
+                        if (tid == 64) tie_check<D, GF>(a, gsc, t - 1, r0, r1, kNW, wg);
                     }
                 }
                 rescan_rest(t);
@@ -1760,10 +1704,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
             else reduce_w0(a.m - 1);
         }
         if (tid == 64 && done == a.m + 1) {
-            if constexpr (!kLanes) {   // (no sweep uses the last winner's row: from the inputs)
+            if constexpr (!kLanes) {
                 WinnerG<D, GF> wg;
                 wg.load(a, gsc, a.m - 1);
-                tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW, wg.g2(), GF ? wg.w : 1.0);
+                tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW, wg);
             }
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)
                 double* st_out = const_cast<double*>(a.tie_bounds) + 2;
