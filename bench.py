@@ -284,8 +284,9 @@ def dedup_timing(prob, m: int, want_idx, stream, repeats: int = 5):
         tie = nat.near_tie_step(ws)
     except nat.HipExtensionError:   # an older A/B build (ST_HIP_LIB) without the guard
         tie = None
-    return {'used': True, 'drop_in_takes_it': bool(prob.guard_mode() == 'kernel' or
-                                                   (prob.dedup_pays(m) and prob.dedup_pays(m, sp.n))),
+    # the drop-in's own rule (DeviceProblem.greedy: dedup_pays before and after detection; the guard does not
+    # force it since round 6 -- repeated rows never flag a step)
+    return {'used': True, 'drop_in_takes_it': bool(prob.dedup_pays(m) and prob.dedup_pays(m, sp.n)),
             'near_tie_step': tie,
             'rows_kept': sp.n, 'of': prob.n, 'detect_s': round(det[-1], 6),
             'thin_s': round(med, 6), 's_per_thin_incl_detect': det[-1] + med,
