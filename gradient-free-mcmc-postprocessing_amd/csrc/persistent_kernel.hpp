@@ -406,6 +406,13 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 #ifndef ST_GUARD_RW0
 #define ST_GUARD_RW0 2
 #endif
+// the near-tie bounds' per-block atomic maxima: spread over this many 64-B slots of the workspace's
+// control block (block b -> slot b % ST_BOUNDS_SLOTS; the late check of step 0 reduces them), or all into the
+// two bounds words (0)
+#ifndef ST_BOUNDS_SLOTS
+#define ST_BOUNDS_SLOTS 16
+#endif
+static_assert(ST_BOUNDS_SLOTS * 64 <= kWsStatusOff, "bounds slots: the control block's first 1 KB");
 #ifndef ST_POLL_SYNC_FIRST
 #define ST_POLL_SYNC_FIRST 1
 #endif
@@ -434,6 +441,13 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 // the same lane advances the threshold recurrence.  Multi-rank runs (nranks > 1): every rank's blocks run
 // the same check against the global winner (each rank flags its own rows; the host combines the ranks'
 // words with one all-reduce after the run) over bounds the host computed from all n rows beforehand.
+
+// slot s of the near-tie bounds' per-block maxima (ST_BOUNDS_SLOTS): 64 B apart in the first kilobyte of the
+// workspace's control block, which st_greedy zeroes with the rest before every launch
+__device__ __forceinline__ uint64_t* bounds_slot(const PersistArgs& a, int s) {
+    char* base = reinterpret_cast<char*>(const_cast<double*>(a.tie_bounds)) - kWsBoundsOff;
+    return reinterpret_cast<uint64_t*>(base + (int64_t)s * 64);
+}
 
 // the row (x, g[, w]) of row r from the read-only inputs
 template <int D, bool GF>
@@ -530,11 +544,20 @@ __device__ __forceinline__ void tie_check(const PersistArgs& a, GuardScratch* sc
     const int par = (int)(t & 1);
     double* ts = sc->tg;   // c1, wmax, Dmax, Q, E, thr
     if (t == 0) {   // stein_ref.c tie_init
-        const uint64_t* bw = reinterpret_cast<const uint64_t*>(a.tie_bounds);
-        const double g2 = __longlong_as_double(
-            (long long)__hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
-        const double w2 = __longlong_as_double(
-            (long long)__hip_atomic_load(bw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        uint64_t* bw = reinterpret_cast<uint64_t*>(const_cast<double*>(a.tie_bounds));
+        uint64_t g2b = __hip_atomic_load(bw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        uint64_t w2b = __hip_atomic_load(bw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#if ST_BOUNDS_SLOTS
+        // the blocks' slots (the words hold the host's all-row bounds of a multi-rank run, else 0): maxima of
+        // non-negative doubles as u64, like the atomics (block 0 writes the result into the words at the end)
+        for (int s = 0; s < ST_BOUNDS_SLOTS; ++s) {
+            const uint64_t* sw = bounds_slot(a, s);
+            g2b = std::max(g2b, (uint64_t)__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            w2b = std::max(w2b, (uint64_t)__hip_atomic_load(sw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        }
+#endif
+        const double g2 = __longlong_as_double((long long)g2b);
+        const double w2 = __longlong_as_double((long long)w2b);
         const double l = a.l, tr = a.tr;
         const double gm = __builtin_sqrt(g2), sl = __builtin_sqrt(l);
         ts[0] = (((3.0 * l + tr) + sl * gm) + 0.5 * l) + 0.5 * g2;
@@ -1117,6 +1140,9 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                 wm = __builtin_fmax(wm, gsc->bnd[w][1]);
             }
             uint64_t* bw = reinterpret_cast<uint64_t*>(const_cast<double*>(a.tie_bounds));
+#if ST_BOUNDS_SLOTS
+            bw = bounds_slot(a, (int)(bid() % ST_BOUNDS_SLOTS));
+#endif
             __hip_atomic_fetch_max(bw, (uint64_t)__double_as_longlong(gm), __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
             __hip_atomic_fetch_max(bw + 1, (uint64_t)__double_as_longlong(wm), __ATOMIC_RELAXED,
@@ -1710,6 +1736,17 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                 tie_check<D, GF>(a, gsc, a.m - 1, r0, r1, kNW, wg);
             }
             if (bid() == 0) {   // block 0's final recurrence state (Q, E, thr(m)) after the bounds (tests)
+#if ST_BOUNDS_SLOTS
+                uint64_t* bw = reinterpret_cast<uint64_t*>(const_cast<double*>(a.tie_bounds));
+                uint64_t g2b = bw[0], w2b = bw[1];
+                for (int s = 0; s < ST_BOUNDS_SLOTS; ++s) {
+                    const uint64_t* sw = bounds_slot(a, s);
+                    g2b = std::max(g2b, (uint64_t)__hip_atomic_load(sw, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                    w2b = std::max(w2b, (uint64_t)__hip_atomic_load(sw + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+                }
+                bw[0] = g2b;   // the bounds the threshold was built from (st_greedy's workspace words)
+                bw[1] = w2b;
+#endif
                 double* st_out = const_cast<double*>(a.tie_bounds) + 2;
                 st_out[0] = gsc->tg[3];
                 st_out[1] = gsc->tg[4];
