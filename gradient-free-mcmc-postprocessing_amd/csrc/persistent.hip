@@ -54,7 +54,10 @@ static int g_persist_cmp = -1;   // st_tune key 12: compact-only kernel register
 // PMC WRITE_SIZE 1.08 GB -> 0.15 GB per thin, but 6.82 -> 6.94-7.01 ms: the 8 B per streamed row take
 // LDS from ~120 LDS rows, which then stream (~1.1 ns instead of ~0.36 ns per row-step), and the A
 // load / store it saves was not on the critical path (L2-resident, stores fire-and-forget).
-static int g_persist_sal = 0;
+// -1 (auto): on under the near-tie guard, whose rescans read every streamed row's sum after each publish --
+// from LDS instead of L2 the guarded all-row config-4 thin takes 9.96 instead of 10.71-10.79 ms (round 6,
+// same box, profiles/r06_guard_knobs.log)
+static int g_persist_sal = -1;
 // st_tune key 16: ticks (10 ns) added to a step's first poll time before it is aligned to the poll
 // grid: -1 auto = 10 for the one-device compact-only kernel, 0 otherwise.  A block whose first poll
 // would fall just before the last records land takes the next grid slot instead of an early,
@@ -143,7 +146,7 @@ int persistent_tune(int key, int value) {
     }
     if (key == 15) {
         if (value < -1 || value > 1) return -1;
-        g_persist_sal = value < 0 ? 0 : value;
+        g_persist_sal = value;
         return 0;
     }
     if (key == 19) {
@@ -350,11 +353,11 @@ static hipError_t plan_persistent(const double* x, const double* g, const double
     const size_t budget = (size_t)(lds_max > 0 ? lds_max : 65536) - 1024;   // static + slack
     // LDS rows (whole 64-row chunks) for rows past the register rows; the 512-thread (dynamic-chunk)
     // kernels also keep every streamed row's running sum in LDS (8 B per row, whole chunks)
-    // (st_tune key 15 = 1 only; when the streamed sums alone would not fit -- more than ~20 000
+    // (st_tune key 15 = 1, or -1 under the near-tie guard; when the streamed sums alone would not fit -- more than ~20 000
     // streamed rows per block -- they stay in HBM: sal = 0)
     auto lds_rows = [&](int nt_, int rt_, int64_t& rl, size_t& bytes, int& sal) {
         const int64_t need_ = R - (int64_t)rt_ * nt_;
-        sal = g_persist_sal == 1 && nt_ == 512 && need_ > 0 &&
+        sal = (g_persist_sal == 1 || (g_persist_sal < 0 && guard)) && nt_ == 512 && need_ > 0 &&
               head + (size_t)(need_ + 63) / 64 * 64 * sizeof(double) <= budget;
         rl = need_ > 0 ? need_ / 64 * 64 : 0;
         if (guard && rl > kGuardLdsRows) rl = kGuardLdsRows;   // the guard's repeat bits (GuardScratch::lrep)
@@ -470,9 +473,9 @@ static hipError_t prepare_ws(Plan& P, hipStream_t s) {
 }
 
 // The near-tie guard's bounds over ALL n rows (stein_ref.c sr_tie_bounds; the staging's operations): a
-// multi-rank run's blocks cover only their rank's rows, so the host merges every row's maxima into the
-// workspace words before the launch -- the blocks' own merges then change nothing, and every rank's
-// threshold recurrence is the single-device one
+// multi-rank run's blocks cover only their rank's rows, so every row's maxima are merged into the workspace's
+// bounds slots before the launch -- the blocks' own merges then change nothing, and every rank's threshold
+// recurrence is the single-device one
 template <int D, bool GF>
 __global__ __launch_bounds__(256) void tie_bounds_kernel(const double* g, const double* w, int64_t n, int64_t ld,
                                                           double* bounds) {
@@ -486,8 +489,18 @@ __global__ __launch_bounds__(256) void tie_bounds_kernel(const double* g, const 
     }
     gm = wave_max_f64(gm);
     wm = wave_max_f64(wm);
-    if ((threadIdx.x & 63) == 0) {
+    // one atomic pair per block, into the block's bounds slot (the persistent blocks' own slots; the late check
+    // of step 0 takes the maximum over the slots and the words): no single contended address
+    __shared__ double wave_m[4][2];
+    if ((threadIdx.x & 63) == 0) { wave_m[threadIdx.x >> 6][0] = gm; wave_m[threadIdx.x >> 6][1] = wm; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (int w = 1; w < 4; ++w) { gm = __builtin_fmax(gm, wave_m[w][0]); wm = __builtin_fmax(wm, wave_m[w][1]); }
         uint64_t* bw = reinterpret_cast<uint64_t*>(bounds);
+#if ST_BOUNDS_SLOTS
+        bw = reinterpret_cast<uint64_t*>(reinterpret_cast<char*>(bounds) - kWsBoundsOff +
+                                         (int64_t)(blockIdx.x % ST_BOUNDS_SLOTS) * 64);
+#endif
         __hip_atomic_fetch_max(bw, (uint64_t)__double_as_longlong(gm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         __hip_atomic_fetch_max(bw + 1, (uint64_t)__double_as_longlong(wm), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

@@ -80,8 +80,9 @@ int64_t st_greedy_workspace_bytes(int64_t n, int32_t d, int32_t nranks);
  * rounding), key 14 = energy-distance work units: grid blocks (256 columns x one B chunk) that
  * st_distance_colsum_ws aims for (256 .. 2^22; -1 = automatic = 32768; the B range is split into
  * that many / ceil(na / 256) chunks of at least 1024 points -- sums within rounding), key 15 = the
- * 512-thread persistent kernels keep the streamed rows' running sums in LDS (1) instead of HBM (0 /
- * -1 = automatic = 0: measured slower; same results), key 16 = persistent kernels:
+ * 512-thread persistent kernels keep the streamed rows' running sums in LDS (1) instead of HBM (0;
+ * -1 = automatic: 1 under the near-tie guard, whose rescans read them every step, else 0 -- measured
+ * slower there; same results), key 16 = persistent kernels:
  * ticks of the 100 MHz s_memrealtime clock added to a step's first winner poll before it is aligned
  * to the chip-wide poll grid (0 .. 450; -1 = automatic = 10 for the one-device compact-only kernel,
  * 0 otherwise;

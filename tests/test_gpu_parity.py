@@ -367,6 +367,36 @@ def test_streamed_sums_in_lds_option(case):
         L.st_tune(5, -1)
 
 
+@pytest.mark.parametrize('case', ['in_range', 'tiny_rows_one_block'])
+def test_streamed_sums_in_lds_guarded(case):
+    """Under the near-tie guard the streamed rows' sums live in LDS by default (st_tune key 15 = -1: the
+    rescans read them every step): the same streamed-row setup as above, guarded, with the key at -1 / 0 --
+    no step flagged, the C model's indices and running sums bit for bit."""
+    from stein_thinning import _native
+    n, m, d = 1_100_003, 30, 4
+    x, g = _rw_chain(n, d, seed=37)
+    s, gs = o._validate_and_standardize(x, g, True)
+    s, gs = s.copy(), gs.copy()
+    if case == 'tiny_rows_one_block':
+        s[500_000:500_010, 1] = 1e-30
+    linv = o.make_precon(s, 'med')
+    l, tr = linv[0, 0], np.trace(linv)
+    prob = DeviceProblem(s, gs, None, l, tr)
+    cidx, cA = oracle_c.greedy_mt(s, gs, None, l, tr, m)
+    L = _native.lib()
+    assert L.st_tune(5, 128) == 0
+    try:
+        for sal in (-1, 0):
+            assert L.st_tune(15, sal) == 0
+            idx, A = prob.greedy(m, return_sums=True, guard=True)
+            assert prob.near_tie == -1, (sal, prob.near_tie)
+            np.testing.assert_array_equal(idx, cidx)
+            assert np.array_equal(A, cA), (sal, np.flatnonzero(A != cA)[:10])
+    finally:
+        L.st_tune(15, -1)
+        L.st_tune(5, -1)
+
+
 @pytest.mark.parametrize('d', [2, 4, 9, 50])
 def test_pair_values_bit_exact_vs_c_model(d):
     x, g = _rw_chain(700, d, seed=100 + d)
