@@ -406,6 +406,17 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 #ifndef ST_GUARD_RW0
 #define ST_GUARD_RW0 2
 #endif
+// the rescan's streamed / LDS row loops unrolled (measurement builds; 1 = the product)
+#ifndef ST_GUARD_UNROLL
+#define ST_GUARD_UNROLL 1
+#endif
+#define ST_PRAGMA_(x) _Pragma(#x)
+#define ST_UNROLL_N_(n) ST_PRAGMA_(unroll n)
+#if ST_GUARD_UNROLL > 1
+#define ST_GUARD_UNROLL_LOOP ST_UNROLL_N_(ST_GUARD_UNROLL)
+#else
+#define ST_GUARD_UNROLL_LOOP
+#endif
 // the near-tie bounds' per-block atomic maxima: spread over this many 64-B slots of the workspace's
 // control block (block b -> slot b % ST_BOUNDS_SLOTS; the late check of step 0 reduces them), or all into the
 // two bounds words (0)
@@ -1089,8 +1100,8 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     if constexpr (GUARD && !kWide) {
         // the problem's bounds for the guard's threshold (stein_ref.c sr_tie_bounds): max_i of
         // g_i0 g_i0 + g_i1 g_i1 + ... and of w_i w_i over this block's rows, a NaN as +inf, merged into the
-        // problem's words with u64 atomic maxima that complete before any record of this block is
-        // published (the fence) -- so a block that has seen every step-0 record sees the final bounds
+        // block's bounds slot (bounds_slot) with u64 atomic maxima that complete before any record of this
+        // block is published (the fence) -- so a block that has seen every step-0 record sees the final bounds
         {
             double gm = 0.0, wm = GF ? 0.0 : 1.0;
             auto take_row = [&](double s2, double wv) {
@@ -1280,6 +1291,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
         if constexpr (!kWide) {
             if (wid >= kRW0) {
                 int j = 0;
+                ST_GUARD_UNROLL_LOOP
                 for (int64_t row = str_base + rt0; row < r1; row += rstep, ++j) {
                     const double av = (kDyn && a.stream_a_lds) ? sA[row - str_base] : a.A[row];
                     o = __builtin_fmin(o, other_of(av, vmin));
@@ -1287,6 +1299,7 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
                     if (j < 32) smsk |= tj ? 1u << j : 0u;
                     else tie |= tj;
                 }
+                ST_GUARD_UNROLL_LOOP
                 for (int e = rt0; e < RL; e += rstep) {
                     const double av = lrow(e)[fA];
                     if (lds_base + e < r1) {
