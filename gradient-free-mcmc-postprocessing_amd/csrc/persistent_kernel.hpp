@@ -406,6 +406,9 @@ __device__ __forceinline__ void publish(const PersistArgs& a, Scratch* sc, doubl
 #ifndef ST_GUARD_RW0
 #define ST_GUARD_RW0 2
 #endif
+#ifndef ST_LANES_W0_IN_POLL
+#define ST_LANES_W0_IN_POLL 1
+#endif
 // the rescan's streamed / LDS row loops unrolled (measurement builds; 1 = the product)
 #ifndef ST_GUARD_UNROLL
 #define ST_GUARD_UNROLL 1
@@ -1027,6 +1030,9 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     GuardScratch* const gsc = reinterpret_cast<GuardScratch*>(lds + (sizeof(Scratch) + 15) / 16 * 2);
     // the per-thread slots of the 256-thread guarded kernels (GuardLanes), after GuardScratch
     constexpr bool kLanes = GUARD && !kDyn && !kWide;
+    // wave 0 rescans its register rows while its first poll is in flight (the 256-thread kernels), or right
+    // after the pick (512 threads; ST_LANES_W0_IN_POLL = 0: the 256-thread kernels too -- measurement builds)
+    constexpr bool kW0InPoll = !kDyn && ST_LANES_W0_IN_POLL;
     GuardLanes* const gl = reinterpret_cast<GuardLanes*>(lds + (sizeof(Scratch) + 15) / 16 * 2 +
                                                          (sizeof(GuardScratch) + 15) / 16 * 2);
     double* const srow0 = lds + (sizeof(Scratch) + 15) / 16 * 2 + (GUARD ? (sizeof(GuardScratch) + 15) / 16 * 2 : 0) +
@@ -1410,10 +1416,10 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     // ---- steps 1 .. m-1 ----------------------------------------------------------------------
     for (; t < a.m; ++t) {
         const int64_t win = wait_and_pick<D, GF, kMaxG, GUARD>(a, sc, t - 1, bid(), G(), gsc, guard,
-                                                               guard && !kDyn, rescan_w0);
+                                                               guard && kW0InPoll, rescan_w0);
         if (win < 0) break;
-        if constexpr (guard && kDyn) {   // wave 0's register rows of step t - 1: per lane into LDS (wave 1
-            if (wid == 0) rescan_w0();   // reduces them after publish(t))
+        if constexpr (guard && !kW0InPoll) {   // wave 0's register rows of step t - 1: per lane into LDS (wave 1
+            if (wid == 0) rescan_w0();         // reduces them after publish(t))
         }
         if (bid() == 0 && tid == 0) a.idx_out[t - 1] = (uint32_t)win;
         // chunk counter of the NEXT step (its last use, step t - 1, ended before publish's barrier)
@@ -1727,14 +1733,14 @@ __global__ __launch_bounds__(NT, BPC) void greedy_persistent(KA ka) {
     int64_t done = t;   // idx[0 .. done-1) are written
     if (t == a.m) {
         const int64_t win = wait_and_pick<D, GF, kMaxG, GUARD>(a, sc, a.m - 1, bid(), G(), gsc, guard,
-                                                               guard && !kDyn, rescan_w0);
+                                                               guard && kW0InPoll, rescan_w0);
         if (win >= 0) {
             if (bid() == 0 && tid == 0) a.idx_out[a.m - 1] = (uint32_t)win;
             done = a.m + 1;
         }
     }
     if constexpr (guard) {
-        if (kDyn && done == a.m + 1) {
+        if (!kW0InPoll && done == a.m + 1) {
             if (wid == 0) rescan_w0();
             __syncthreads();
         }
